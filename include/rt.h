@@ -1,0 +1,335 @@
+/*
+ * rt.h — C ABI of the MI355X-native path tracer (drop-in for the render path of
+ * shaunplee/ray-tracing).
+ *
+ * The reference has no FFI: its render boundary is the pure Haskell call
+ *     runRender :: RenderStaticEnv -> [RandGen] -> [VV.Vector RGB]     (src/Lib.hs:1491)
+ * with the environment built by
+ *     mkRenderStaticEnv scene camera (w,h) ns maxDepth nThreads        (src/Lib.hs:92-108)
+ * and   type Scene = (Hittable world, Hittable lights, Albedo background)  (src/Lib.hs:84).
+ * This header replaces that call with plain C: the immutable Haskell `Scene` becomes a
+ * flattened `rt_scene_desc` (arrays of POD records), the `Camera` becomes `rt_camera`,
+ * `[RandGen]` becomes an array of SplitMix64 (seed, gamma) pairs, and the lazily streamed
+ * `[Vector RGB]` becomes a caller-owned H*W*3 byte buffer (top row first, PPM order).
+ *
+ * Scene construction (Lib.hs constructors, makeBVH, makePerlin, Scenes.hs builders and
+ * cameras) is exported too (rt_builder_*, rt_scene_named, rt_camera_*), so a host that
+ * used the reference's Scenes.hs API finds the same surface here.
+ *
+ * Conventions: every function returns 0 on success and a negative RT_E* code on error;
+ * the message is available from rt_last_error() (thread-local). No torch / C++ types.
+ */
+#ifndef RT_H
+#define RT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* ------------------------------------------------------------------ error codes */
+#define RT_OK 0
+#define RT_E_INVALID (-1)   /* bad argument / malformed scene                       */
+#define RT_E_HIP (-2)       /* HIP runtime error                                     */
+#define RT_E_NOMEM (-3)     /* allocation failure                                    */
+#define RT_E_UNSUPPORTED (-4)/* scene uses a construct the device path does not take */
+#define RT_E_STATE (-5)     /* call order (e.g. render before upload)                */
+
+/* ------------------------------------------------------------------ scene records */
+
+/* Flattened `Hittable` (src/Lib.hs:521-585). One 64-byte record per constructor. */
+enum rt_node_type {
+    RT_NODE_BVH = 0,             /* BVHNode left right box size        (Lib.hs:552-560) */
+    RT_NODE_SPHERE = 1,          /* Sphere center radius material      (Lib.hs:522-528) */
+    RT_NODE_MOVING_SPHERE = 2,   /* MovingSphere c0 c1 t0 t1 dur r mat (Lib.hs:529-543) */
+    RT_NODE_RECT_XY = 3,         /* Rect (XYRect x0 x1 y0 y1 k mat)    (Lib.hs:608-620) */
+    RT_NODE_RECT_XZ = 4,         /* Rect (XZRect x0 x1 z0 z1 k mat)    (Lib.hs:621-633) */
+    RT_NODE_RECT_YZ = 5,         /* Rect (YZRect y0 y1 z0 z1 k mat)    (Lib.hs:634-646) */
+    RT_NODE_CUBOID = 6,          /* Cuboid min max [6 rects]           (Lib.hs:545-551,594-605) */
+    RT_NODE_TRANSLATE = 7,       /* Translate offset child             (Lib.hs:561-565) */
+    RT_NODE_ROTATE = 8,          /* Rotate axis sin cos box child      (Lib.hs:566-576) */
+    RT_NODE_CONSTANT_MEDIUM = 9, /* ConstantMedium (-1/density) mat boundary (Lib.hs:577-583) */
+    RT_NODE_UNHITTABLE = 10,     /* Unhittable                         (Lib.hs:584) */
+    RT_NODE_EXT = 11             /* payload continuation of the previous record (never a child) */
+};
+
+/*
+ * Field use per type (f = 6 doubles, a/b/c = int32):
+ *   BVH            f = box min xyz, box max xyz;   a = left, b = right
+ *   SPHERE         f[0..2] = center, f[3] = radius; a = material
+ *   MOVING_SPHERE  f[0..2] = center0, f[3..5] = center1; a = material;
+ *                  the next record (type EXT) holds f[0]=time0, f[1]=time1, f[2]=duration, f[3]=radius
+ *   RECT_XY/XZ/YZ  f[0..4] = (i0, i1, j0, j1, k) in the constructor's argument order; a = material
+ *   CUBOID         f = min xyz, max xyz; a = material (the six rects are implied, Lib.hs:599-604)
+ *   TRANSLATE      f[0..2] = offset; a = child
+ *   ROTATE         f[0] = sin theta, f[1] = cos theta; a = child; b = axis (0 X, 1 Y, 2 Z)
+ *   CONSTANT_MEDIUM f[0] = negative inverse density; a = boundary; b = phase material
+ * For every type c = htblSize of the node (Lib.hs:662-671): BVH its size, Translate/Rotate
+ * the size of the child, Unhittable 0, everything else 1.
+ */
+typedef struct rt_node {
+    double f[6];
+    int32_t type;
+    int32_t a;
+    int32_t b;
+    int32_t c;
+} rt_node; /* 64 bytes */
+
+/* `Material` (src/Lib.hs:339-345). */
+enum rt_material_type {
+    RT_MAT_LAMBERTIAN = 0,
+    RT_MAT_METAL = 1,
+    RT_MAT_DIELECTRIC = 2,
+    RT_MAT_DIFFUSE_LIGHT = 3,
+    RT_MAT_ISOTROPIC = 4
+};
+
+typedef struct rt_material {
+    int32_t type;
+    int32_t texture; /* texture id (Lambertian, Metal, DiffuseLight, Isotropic) */
+    double param;    /* Metal: fuzz; Dielectric: refractive index */
+} rt_material;       /* 16 bytes */
+
+/* `Texture` (src/Lib.hs:394-419). */
+enum rt_texture_type {
+    RT_TEX_CONSTANT = 0, /* f[0..2] = albedo */
+    RT_TEX_CHECKER = 1,  /* a = odd texture, b = even texture */
+    RT_TEX_PERLIN = 2,   /* a = perlin table id, f[0] = scale */
+    RT_TEX_IMAGE = 3     /* a = image id (-1 = Nothing), b = width, c = height */
+};
+
+typedef struct rt_texture {
+    int32_t type;
+    int32_t a;
+    int32_t b;
+    int32_t c;
+    double f[4];
+} rt_texture; /* 48 bytes */
+
+/* Perlin tables of `makePerlin` (src/Lib.hs:424-439). */
+typedef struct rt_perlin {
+    double ranvec[256][3];
+    int32_t perm_x[256];
+    int32_t perm_y[256];
+    int32_t perm_z[256];
+} rt_perlin; /* 9216 bytes */
+
+/* RGB8 raster (the JuicyPixels `Image PixelRGB8` of src/Lib.hs:384-389), row-major, row 0 = top. */
+typedef struct rt_image {
+    int64_t offset; /* byte offset into rt_scene_desc.image_pool */
+    int32_t width;
+    int32_t height;
+} rt_image;
+
+typedef struct rt_scene_desc {
+    const rt_node* nodes;
+    int32_t n_nodes;
+    int32_t world_root;  /* node id of the world Hittable */
+    int32_t lights_root; /* node id of the lights Hittable; -1 = Unhittable */
+    int32_t n_materials;
+    const rt_material* materials;
+    const rt_texture* textures;
+    int32_t n_textures;
+    int32_t n_perlins;
+    const rt_perlin* perlins;
+    const rt_image* images;
+    int32_t n_images;
+    int32_t _pad;
+    const uint8_t* image_pool;
+    int64_t image_pool_bytes;
+    double background[3]; /* Albedo background (src/Lib.hs:84) */
+} rt_scene_desc;
+
+/* `Camera` (src/Lib.hs:1230-1251), as computed by newCamera (src/Lib.hs:1280-1295). */
+typedef struct rt_camera {
+    double origin[3];
+    double llc[3];
+    double horiz[3];
+    double vert[3];
+    double u[3];
+    double v[3];
+    double w[3];
+    double lens_radius;
+    double t0;
+    double t1;
+} rt_camera;
+
+/* ------------------------------------------------------------------ render parameters */
+
+/*
+ * RNG stream layouts.
+ *  RT_RNG_EXACT  (tier A): the reference's layout — one SplitMix64 generator per image
+ *                column, threaded top row to bottom row, through every sample and bounce
+ *                (src/Lib.hs:1491-1523, 1352-1371). Only width-parallel.
+ *  RT_RNG_PHILOX (tier B): one Philox4x32-10 stream per (pixel, sample), key = seed,
+ *                counter = {draw_pair, sample, pixel_id, 0}; each 128-bit block yields two
+ *                64-bit words, converted exactly as random-1.2.0 `random :: Double`.
+ *                Samples are summed in sample order. Embarrassingly parallel.
+ */
+#define RT_RNG_EXACT 0
+#define RT_RNG_PHILOX 1
+
+/* Flags. */
+#define RT_FLAG_NAN_CULL 1u /* tier B only: stop tracing a pixel once its sum is NaN
+                               (its output byte is then fixed at 0, src/Lib.hs:287-288).
+                               Output-identical; off by default. */
+
+typedef struct rt_render_params {
+    int32_t width;
+    int32_t height;
+    int32_t spp;       /* numSamples */
+    int32_t max_depth; /* maxDepth */
+    int32_t rng_mode;  /* RT_RNG_EXACT | RT_RNG_PHILOX */
+    uint32_t flags;
+    uint64_t seed;       /* tier B Philox key */
+    int32_t tile;        /* tile edge in pixels for sharding (0 = default 16) */
+    int32_t shard_rank;  /* this shard (0-based) */
+    int32_t shard_count; /* number of shards (GPUs); tiles are dealt round-robin */
+    int32_t _pad;
+} rt_render_params;
+
+/* ------------------------------------------------------------------ version / errors */
+int rt_abi_version(void);
+const char* rt_last_error(void);
+
+/* ------------------------------------------------------------------ RNG (src/Random.hs) */
+/* randGen s = mkStdGen s  (src/Random.hs:20-21): writes (seed, gamma). */
+void rt_rand_gen(int64_t s, uint64_t out_gen[2]);
+/* randomDouble (src/Random.hs:23-25): one draw, advances gen in place. */
+double rt_random_double(uint64_t gen[2]);
+
+/* ------------------------------------------------------------------ scene construction */
+/* A builder owns the RandGen threaded through scene construction (makeBVH / makePerlin
+ * draw from it, src/Lib.hs:941-943, 424-439) and the growing record arrays. Object ids
+ * returned by the constructors are node ids. */
+typedef struct rt_builder rt_builder;
+
+int rt_builder_create(const uint64_t gen[2], rt_builder** out);
+void rt_builder_destroy(rt_builder* b);
+/* Current generator state (the `g1` handed back by the Scenes.hs builders). */
+void rt_builder_gen(const rt_builder* b, uint64_t out_gen[2]);
+
+int rt_tex_constant(rt_builder* b, double r, double g, double bl);
+int rt_tex_checker(rt_builder* b, int odd_tex, int even_tex);
+int rt_tex_perlin(rt_builder* b, double scale); /* makePerlin: consumes 768 + 3*255 draws */
+int rt_tex_image(rt_builder* b, const uint8_t* rgb, int width, int height); /* rgb NULL = Nothing */
+
+int rt_mat_lambertian(rt_builder* b, int tex);
+int rt_mat_metal(rt_builder* b, int tex, double fuzz);
+int rt_mat_dielectric(rt_builder* b, double ref_idx);
+int rt_mat_diffuse_light(rt_builder* b, int tex);
+int rt_mat_isotropic(rt_builder* b, int tex);
+
+int rt_obj_sphere(rt_builder* b, const double center[3], double radius, int mat);
+int rt_obj_moving_sphere(rt_builder* b, const double c0[3], const double c1[3], double t0, double t1,
+                         double radius, int mat);
+/* plane: 0 = XYPlane, 1 = XZPlane, 2 = YZPlane (src/Lib.hs:649-660) */
+int rt_obj_rect(rt_builder* b, int plane, double a0, double a1, double b0, double b1, double k, int mat);
+int rt_obj_cuboid(rt_builder* b, const double pmin[3], const double pmax[3], int mat);
+int rt_obj_translate(rt_builder* b, const double offset[3], int child);
+int rt_obj_rotate(rt_builder* b, int axis, double angle_deg, int child);
+int rt_obj_constant_medium(rt_builder* b, double density, int tex, int boundary);
+int rt_obj_unhittable(rt_builder* b);
+/* makeBVH mtime items (src/Lib.hs:941-961); has_time = 0 for Nothing. Consumes draws. */
+int rt_obj_bvh(rt_builder* b, const int* items, int n_items, int has_time, double t0, double t1);
+
+/* Seal the scene: world root, lights root (-1 = Unhittable), background. The descriptor
+ * points into builder-owned memory and stays valid until the builder is destroyed. */
+int rt_builder_finish(rt_builder* b, int world, int lights, const double background[3],
+                      rt_scene_desc* out_desc);
+
+/* Named scenes of src/Scenes.hs (ids below). `earth` = ImageTexture raster or NULL (Nothing).
+ * The builder must be fresh; its generator is threaded as in the reference. */
+enum rt_scene_id {
+    RT_SCENE_CORNELL_BOX = 0,       /* makeCornellBoxScene        Scenes.hs:32-73   */
+    RT_SCENE_CORNELL_SMOKE = 1,     /* makeCornellSmokeBoxScene   Scenes.hs:75-118  */
+    RT_SCENE_SIMPLE_LIGHT = 2,      /* makeSimpleLightScene       Scenes.hs:133-155 */
+    RT_SCENE_EARTH = 3,             /* makeEarthScene             Scenes.hs:167-179 */
+    RT_SCENE_TWO_PERLIN_SPHERES = 4,/* makeTwoPerlinSpheresScene  Scenes.hs:194-211 */
+    RT_SCENE_TWO_SPHERES = 5,       /* makeTwoSpheresScene        Scenes.hs:213-237 */
+    RT_SCENE_RANDOM_BOOK_ONE = 6,   /* makeRandomSceneBookOne     Scenes.hs:253-317 */
+    RT_SCENE_RANDOM = 7,            /* makeRandomScene            Scenes.hs:321-399 */
+    RT_SCENE_NEXT_WEEK_FINAL = 8,   /* makeNextWeekFinalScene     Scenes.hs:414-466 */
+    RT_SCENE_THREE_SPHERES = 9,     /* config 1: ground + s1..s3 of Scenes.hs:263-279, BVH (0,1) */
+    RT_SCENE_STRESS_SPHERES = 10    /* config 5: `param` random spheres + ground, BVH (0,1) */
+};
+int rt_scene_named(rt_builder* b, int scene_id, double t0, double t1, const uint8_t* earth_rgb,
+                   int earth_w, int earth_h, int64_t param, rt_scene_desc* out_desc);
+
+/* newCamera lookfrom lookat vup vfov aspect aperture focusDist t0 t1 (src/Lib.hs:1269-1295). */
+void rt_camera_new(const double lookfrom[3], const double lookat[3], const double vup[3], double vfov,
+                   double aspect, double aperture, double focus_dist, double t0, double t1,
+                   rt_camera* out);
+enum rt_camera_id {
+    RT_CAM_CORNELL = 0,      /* cornellCamera             Scenes.hs:120-131 */
+    RT_CAM_TWO_SPHERES = 1,  /* twoSpheresSceneCamera     Scenes.hs:181-192 */
+    RT_CAM_RANDOM_SCENE = 2, /* randomSceneCamera         Scenes.hs:239-250 */
+    RT_CAM_NEXT_WEEK = 3     /* nextWeekFinalSceneCamera  Scenes.hs:401-412 */
+};
+int rt_camera_named(int cam_id, int width, int height, rt_camera* out);
+
+/* P3 PPM text exactly as app/Main.hs:59-61 + printRow/showRow (src/Lib.hs:299-305).
+ * Writes at most cap bytes; *out_len = bytes required. */
+int rt_write_ppm(const uint8_t* rgb, int width, int height, char* buf, size_t cap, size_t* out_len);
+
+/* ------------------------------------------------------------------ device path */
+typedef struct rt_ctx rt_ctx;
+
+int rt_device_count(int* out);
+/* Bind one HIP device (one process per GPU). */
+int rt_create(int device, rt_ctx** out);
+void rt_destroy(rt_ctx* ctx);
+/* Copy a scene to device memory (caller-owned desc; arrays are copied). Validates it. */
+int rt_upload_scene(rt_ctx* ctx, const rt_scene_desc* desc);
+
+/*
+ * Blocking full-image render (replaces runRender, src/Lib.hs:1491).
+ *   col_gens     tier A: 2*width words (seed, gamma) per column, column 0 first
+ *                (app/Main.hs:47-49); ignored in tier B.
+ *   out_rgb8     H*W*3 bytes, top row first (pixelPositions, src/Lib.hs:1488-1489).
+ *   out_linear   optional H*W*3 doubles: the per-pixel average before albedoToColor.
+ *   out_col_gens optional (tier A): generators after the last row, 2*width words.
+ * shard_rank/shard_count in params are ignored (whole image).
+ */
+int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* p, const uint64_t* col_gens,
+              uint8_t* out_rgb8, double* out_linear, uint64_t* out_col_gens);
+
+/*
+ * Multi-GPU building blocks (tier B only). The image is cut into tile x tile squares,
+ * numbered row-major from the top-left; shard r owns tiles r, r+N, r+2N, ... and writes
+ * them into a "slab": tiles_per_shard * tile * tile pixels, tile-major. Every shard's slab
+ * has the same size (padded), so slabs can be all-gathered as-is.
+ */
+int rt_shard_geometry(const rt_render_params* p, int64_t* tiles_total, int64_t* tiles_per_shard,
+                      int64_t* slab_pixels);
+/* Render this shard into device buffers on `stream` (hipStream_t, NULL = default).
+ * d_slab_rgb8: slab_pixels*3 bytes; d_slab_linear: slab_pixels*3 doubles or NULL.
+ * Asynchronous: stream-ordered, returns after the launches are queued. */
+int rt_render_shard_async(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* p,
+                          uint8_t* d_slab_rgb8, double* d_slab_linear, void* stream);
+/* Scatter shard_count gathered slabs (concatenated, rank-major) into a H*W*3 device image. */
+int rt_assemble_async(rt_ctx* ctx, const rt_render_params* p, const uint8_t* d_slabs_rgb8,
+                      uint8_t* d_image_rgb8, void* stream);
+/* Same for the optional linear (double) slabs. */
+int rt_assemble_linear_async(rt_ctx* ctx, const rt_render_params* p, const double* d_slabs_linear,
+                             double* d_image_linear, void* stream);
+
+/* Timing of the last render launch on this ctx (HIP events on the launch stream), ms. */
+int rt_last_kernel_ms(rt_ctx* ctx, double* out_ms);
+
+/*
+ * Debug / parity entry: closest hit of n world rays (7 doubles each: origin, direction, time)
+ * in [tmin, tmax]. out: 12 doubles per ray: hit(0/1), t, p xyz, normal xyz, u, v, front_face,
+ * material. Media draws use tier-B stream (seed, pixel_id = ray index, sample 0).
+ */
+int rt_debug_closest_hits(rt_ctx* ctx, const double* rays, int n, double tmin, double tmax,
+                          uint64_t seed, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_H */

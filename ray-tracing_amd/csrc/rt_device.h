@@ -1,0 +1,251 @@
+// rt_device.h — device-side geometry, RNG and shading for the gfx950 path tracer.
+//
+// Everything here is fp64 and compiled with -ffp-contract=off: the reference is Haskell on
+// GHC 8.8's x86-64 NCG (no FMA), and its semantics are followed operation by operation
+// (evaluation order of `infixl 7` vector ops, GHC's NaN-propagating min/max, strict/lenient
+// interval tests per primitive). Every function cites the src/Lib.hs lines it follows.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rt.h"
+
+#ifndef RT_BLOCK
+#define RT_BLOCK 128 /* threads per workgroup (2 waves) */
+#endif
+#ifndef RT_STACK
+#define RT_STACK 32 /* traversal stack entries per lane (LDS) */
+#endif
+#define RT_LIGHT_DEPTH 2  /* max BVH depth of the lights tree (host-validated) */
+#define RT_FRAME 0x40000000 /* stack-entry tag: instance frame marker */
+#define RT_CHAIN_PRIM 0x100 /* device node type flag: Translate/Rotate chain ending in a primitive */
+#define RT_TYPE_MASK 0xff
+
+namespace rtd {
+
+constexpr double kEps = 0.0001;            // src/Lib.hs:76-77
+constexpr double kPi = 3.141592653589793;  // GHC pi
+
+struct V3 {
+  double x, y, z;
+};
+__device__ __forceinline__ V3 v3(double x, double y, double z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 vmul(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ V3 vneg(V3 a) { return v3(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ V3 scale(double k, V3 a) { return v3(a.x * k, a.y * k, a.z * k); }
+__device__ __forceinline__ V3 divide(V3 a, double k) { return v3(a.x / k, a.y / k, a.z / k); }
+__device__ __forceinline__ double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+  return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ double sqlen(V3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+__device__ __forceinline__ double vlen(V3 a) { return sqrt(sqlen(a)); }
+__device__ __forceinline__ V3 unit(V3 a) { return divide(a, vlen(a)); }
+__device__ __forceinline__ V3 vload(const double* p) { return v3(p[0], p[1], p[2]); }
+__device__ __forceinline__ double comp(V3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+// GHC Ord defaults: max x y = if x <= y then y else x; min x y = if x <= y then x else y.
+__device__ __forceinline__ double gmax(double x, double y) { return x <= y ? y : x; }
+__device__ __forceinline__ double gmin(double x, double y) { return x <= y ? x : y; }
+
+struct Ray {
+  V3 o, d;
+  double tm;
+};
+struct Hit {
+  double t;
+  V3 p, n;
+  double u, v;
+  int ff;
+  int mat;
+};
+__device__ __forceinline__ V3 at(const Ray& r, double t) { return r.o + scale(t, r.d); }  // Lib.hs:317-318
+
+// Device material: the rt_material record plus whether its texture tree reads (u, v).
+struct DMat {
+  int type;
+  int tex;
+  double param;
+  int needs_uv;
+  int _pad;
+};
+
+struct Scene {
+  const rt_node* nodes;
+  const DMat* mats;
+  const rt_texture* texs;
+  const rt_perlin* perlins;
+  const rt_image* images;
+  const uint8_t* pool;
+  int world;
+  int lights;
+  double bg[3];
+};
+
+// ------------------------------------------------------------------ RNG
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 33)) * 0xff51afd7ed558ccdULL;
+  z = (z ^ (z >> 33)) * 0xc4ceb9fe1a85ec53ULL;
+  return z ^ (z >> 33);
+}
+// random-1.2.0 `random :: Double` = 1 - word64/2^64 (src/Random.hs:23-25)
+__device__ __forceinline__ double word_to_draw(uint64_t w) {
+  return 1.0 - (double)w / 18446744073709551616.0;
+}
+
+// Tier A: the reference's SplitMix64 stream (nextWord64).
+struct RngExact {
+  uint64_t seed, gamma;
+  __device__ __forceinline__ double draw() {
+    seed += gamma;
+    return word_to_draw(mix64(seed));
+  }
+};
+
+// Tier B: Philox4x32-10, key = seed, counter = {pair, sample, pixel, 0}; two draws per block.
+__device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+    const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0;
+    c[1] = lo1;
+    c[2] = n2;
+    c[3] = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+struct RngPhilox {
+  uint32_t k0, k1, pid, sample, pair;
+  uint32_t have;
+  uint64_t spare;
+  __device__ __forceinline__ void init(uint64_t seed, uint32_t p, uint32_t s) {
+    k0 = (uint32_t)seed;
+    k1 = (uint32_t)(seed >> 32);
+    pid = p;
+    sample = s;
+    pair = 0;
+    have = 0;
+    spare = 0;
+  }
+  __device__ __forceinline__ double draw() {
+    uint64_t w;
+    if (have) {
+      have = 0;
+      w = spare;
+    } else {
+      uint32_t c[4] = {pair, sample, pid, 0u};
+      philox(c, k0, k1);
+      ++pair;
+      w = (uint64_t)c[0] | ((uint64_t)c[1] << 32);
+      spare = (uint64_t)c[2] | ((uint64_t)c[3] << 32);
+      have = 1;
+    }
+    return word_to_draw(w);
+  }
+};
+
+template <class R>
+__device__ __forceinline__ double draw_r(R& g, double mn, double mx) {  // randomDoubleRM
+  const double rd = g.draw();
+  return mn + (mx - mn) * rd;
+}
+template <class R>
+__device__ __forceinline__ V3 random_in_unit_sphere(R& g) {  // Lib.hs:1160-1168
+  for (;;) {
+    const double x = g.draw(), y = g.draw(), z = g.draw();
+    const V3 p = scale(2.0, v3(x, y, z)) - v3(1.0, 1.0, 1.0);
+    if (sqlen(p) < 1.0) return p;
+  }
+}
+template <class R>
+__device__ __forceinline__ V3 random_in_unit_disk(R& g) {  // Lib.hs:1178-1185
+  for (;;) {
+    const double x = g.draw(), y = g.draw();
+    const V3 p = scale(2.0, v3(x, y, 0.0)) - v3(1.0, 1.0, 0.0);
+    if (sqlen(p) < 1.0) return p;
+  }
+}
+template <class R>
+__device__ __forceinline__ V3 random_unit_vector(R& g) {  // Lib.hs:1187-1197
+  const double aa = g.draw();
+  const double a = aa * 2.0 * kPi;
+  const double zz = g.draw();
+  const double z = (zz * 2.0) - 1.0;
+  const double r = sqrt(1.0 - z * z);
+  return v3(r * cos(a), r * sin(a), z);
+}
+template <class R>
+__device__ __forceinline__ V3 random_cosine_direction(R& g) {  // Lib.hs:1206-1217
+  const double r1 = g.draw(), r2 = g.draw();
+  const double z = sqrt(1.0 - r2);
+  const double phi = 2.0 * kPi * r1;
+  const double sr2 = sqrt(r2);
+  return v3(cos(phi) * sr2, sin(phi) * sr2, z);
+}
+template <class R>
+__device__ __forceinline__ V3 random_to_sphere(R& g, double radius, double dist_squared) {  // Lib.hs:1219-1228
+  const double r1 = g.draw(), r2 = g.draw();
+  const double z = 1.0 + r2 * (sqrt(1.0 - radius * radius / dist_squared) - 1.0);
+  const double phi = 2.0 * kPi * r1;
+  const double s = sqrt(1.0 - z * z);
+  return v3(cos(phi) * s, sin(phi) * s, z);
+}
+
+// ------------------------------------------------------------------ ONB (Lib.hs:263-279)
+struct ONB {
+  V3 u, v, w;
+};
+__device__ __forceinline__ ONB onb_from_w(V3 n) {
+  ONB o;
+  o.w = unit(n);
+  const V3 a = fabs(o.w.x) > 0.9 ? v3(0.0, 1.0, 0.0) : v3(1.0, 0.0, 0.0);
+  o.v = unit(cross(o.w, a));
+  o.u = cross(o.w, o.v);
+  return o;
+}
+__device__ __forceinline__ V3 onb_local(const ONB& o, V3 a) {
+  return (scale(a.x, o.u) + scale(a.y, o.v)) + scale(a.z, o.w);
+}
+
+// GHC's RealFloat-default atan2 (GHC.Float), used by `hit Sphere` for u (Lib.hs:1102).
+__device__ __forceinline__ bool neg_zero(double x) { return x == 0.0 && signbit(x); }
+__device__ inline double ghc_atan2(double y, double x) {
+  double sgn = 1.0;
+  // -atan2 (-y) x branch, applied at most once (it maps y < 0 to y > 0 / y = +0)
+  if ((x <= 0 && y < 0) || (x < 0 && neg_zero(y)) || (neg_zero(x) && neg_zero(y))) {
+    sgn = -1.0;
+    y = -y;
+  }
+  double r;
+  if (x > 0) r = atan(y / x);
+  else if (x == 0 && y > 0) r = kPi / 2;
+  else if (x < 0 && y > 0) r = kPi + atan(y / x);
+  else if (y == 0 && (x < 0 || neg_zero(x))) r = kPi;
+  else if (x == 0 && y == 0) r = y;
+  else r = x + y;
+  return sgn * r;
+}
+
+// faceNormal (Lib.hs:1111-1117)
+__device__ __forceinline__ void face_normal(const Ray& r, V3 outward, int& ff, V3& n) {
+  ff = dot(r.d, outward) < 0;
+  n = ff ? outward : vneg(outward);
+}
+
+// rotatePoint / unRotatePoint (Lib.hs:763-787)
+__device__ __forceinline__ V3 rotate_point(int axis, double s, double c, V3 p) {
+  if (axis == 0) return v3(p.x, c * p.y - s * p.z, s * p.y + c * p.z);
+  if (axis == 1) return v3(c * p.x + s * p.z, p.y, -s * p.x + c * p.z);
+  return v3(c * p.x - s * p.y, s * p.x + c * p.y, p.z);
+}
+__device__ __forceinline__ V3 unrotate_point(int axis, double s, double c, V3 p) {
+  if (axis == 0) return v3(p.x, c * p.y + s * p.z, -s * p.y + c * p.z);
+  if (axis == 1) return v3(c * p.x - s * p.z, p.y, s * p.x + c * p.z);
+  return v3(c * p.x + s * p.y, -s * p.x + c * p.y, p.z);
+}
+
+}  // namespace rtd

@@ -1,0 +1,810 @@
+// rt_render.hip — render kernels for gfx950 and the device half of the C ABI (include/rt.h).
+//
+// Kernel design:
+//  * one work-item = one pixel; a lane keeps its pixel until all `spp` samples are summed, in
+//    sample order, so each pixel's sum is formed exactly as renderPos does (Lib.hs:1343-1350);
+//  * persistent waves with path regeneration: every loop iteration traces ONE segment for every
+//    live lane; a lane whose path ended starts its next sample (or fetches a new pixel through
+//    one wave-aggregated atomicAdd on a work counter) at the top of the next iteration, so
+//    lanes never idle waiting for the longest path of a sample;
+//  * forward throughput (thr *= att * (spdf / pdf)) instead of the reference's continuation;
+//    colour never feeds control flow or the RNG, so this changes rounding only;
+//  * the BVH traversal stack lives in LDS, [entry][lane] so consecutive lanes hit consecutive
+//    banks;
+//  * tier B (Philox per (pixel, sample)) shards by tiles with no data-path collective; tier A
+//    (the reference's per-column SplitMix stream) runs one lane per column.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rt.h"
+#include "rt_device.h"
+#include "rt_internal.h"
+#include "rt_trace.h"
+
+using namespace rtd;
+
+namespace {
+
+struct RenderArgs {
+  Scene S;
+  rt_camera cam;
+  int W, H, spp, max_depth;
+  uint32_t flags;
+  int tile, tiles_x, tiles_total, shard_rank, shard_count;
+  long long work_total;  // slab pixels of this shard
+  uint64_t seed;
+  unsigned long long* counter;
+  uint8_t* out_rgb;  // tier B: slab; tier A: image
+  double* out_lin;
+  uint64_t* gens;  // tier A: per-column (seed, gamma), updated in place
+};
+
+// Slab work index -> image pixel (tile-major, 8x8 blocks inside a tile).
+__device__ __forceinline__ bool work_pixel(const RenderArgs& A, long long w, int& px, int& row) {
+  const long long tp = (long long)A.tile * A.tile;
+  const long long lt = w / tp;
+  const int within = (int)(w - lt * tp);
+  const long long gt = (long long)A.shard_rank + lt * A.shard_count;
+  if (gt >= A.tiles_total) return false;
+  const int tx = (int)(gt % A.tiles_x), ty = (int)(gt / A.tiles_x);
+  const int bpr = A.tile >> 3;
+  const int blk = within >> 6, l = within & 63;
+  px = tx * A.tile + (blk % bpr) * 8 + (l & 7);
+  row = ty * A.tile + (blk / bpr) * 8 + (l >> 3);
+  return px < A.W && row < A.H;
+}
+
+// getRay (Lib.hs:1253-1267): the disk and time draws always happen.
+template <class R>
+__device__ __forceinline__ Ray get_ray(const rt_camera& k, double s, double t, R& g) {
+  const V3 rd = scale(k.lens_radius, random_in_unit_disk(g));
+  const V3 offset = scale(rd.x, vload(k.u)) + scale(rd.y, vload(k.v));
+  const double tm = draw_r(g, k.t0, k.t1);
+  Ray r;
+  r.o = vload(k.origin) + offset;
+  r.d = (((vload(k.llc) + scale(s, vload(k.horiz))) + scale(t, vload(k.vert))) - vload(k.origin)) - offset;
+  r.tm = tm;
+  return r;
+}
+
+// scaleColor (Lib.hs:287-288): NaN -> 0, +inf -> 255.
+__device__ __forceinline__ uint8_t scale_color(double x) {
+  const double s = sqrt(x);
+  const double cl = s < 0.0 ? 0.0 : (s > 0.999 ? 0.999 : s);
+  const double f = floor(256 * cl);
+  return f == f ? (uint8_t)(int)f : (uint8_t)0;
+}
+
+__device__ __forceinline__ void store_pixel(const RenderArgs& A, long long idx, V3 avg) {
+  A.out_rgb[idx * 3 + 0] = scale_color(avg.x);
+  A.out_rgb[idx * 3 + 1] = scale_color(avg.y);
+  A.out_rgb[idx * 3 + 2] = scale_color(avg.z);
+  if (A.out_lin) {
+    A.out_lin[idx * 3 + 0] = avg.x;
+    A.out_lin[idx * 3 + 1] = avg.y;
+    A.out_lin[idx * 3 + 2] = avg.z;
+  }
+}
+
+// One path segment: closest hit, then emission/background or a scatter. Returns true when the
+// path ends, with its contribution in `contrib` (rayColor, Lib.hs:1298-1333).
+template <unsigned F, class R>
+__device__ __forceinline__ bool segment(const RenderArgs& A, Ray& ray, V3& thr, int& depth, R& g, int* stk,
+                                        V3& contrib) {
+  const Scene& S = A.S;
+  if (depth <= 0) {  // d <= 0 -> black
+    contrib = vmul(thr, v3(0.0, 0.0, 0.0));
+    return true;
+  }
+  Hit h;
+  if (!traverse<F>(S, S.world, ray, kEps, INFINITY, h, g, stk)) {
+    contrib = vmul(thr, v3(S.bg[0], S.bg[1], S.bg[2]));
+    return true;
+  }
+  const DMat m = S.mats[h.mat];
+  if (m.type == RT_MAT_DIFFUSE_LIGHT) {  // scatter -> Nothing: emitted (Lib.hs:880-885)
+    const V3 e = h.ff ? v3(0, 0, 0) : texture_value<F>(S, m.tex, h.u, h.v, h.p);
+    contrib = vmul(thr, e);
+    return true;
+  }
+  Scatter s;
+  scatter<F>(S, m, ray, h, g, s);
+  if (s.specular) {
+    thr = vmul(thr, s.att);
+  } else {
+    const double c = dot(h.n, s.ray.d);  // scatteringPdf (Lib.hs:874-878)
+    const double spdf = c < 0 ? 0 : c / kPi;
+    const double k = spdf / s.pdf;
+    thr = vmul(thr, scale(k, s.att));
+  }
+  ray = s.ray;
+  --depth;
+  return false;
+}
+
+// ---------------------------------------------------------------- tier B: Philox per (pixel, sample)
+template <unsigned F>
+__global__ void __launch_bounds__(RT_BLOCK) render_philox(RenderArgs A) {
+  __shared__ int stk_mem[RT_STACK * RT_BLOCK];
+  int* stk = &stk_mem[threadIdx.x];
+  const int lane = threadIdx.x & 63;
+  const unsigned long long lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+  long long w = -1;
+  bool done = false, path = false;
+  int px = 0, row = 0, s = 0, depth = 0;
+  Ray ray;
+  V3 thr = v3(0, 0, 0), sum = v3(0, 0, 0);
+  RngPhilox g;
+  g.init(A.seed, 0, 0);
+
+  for (;;) {
+    // acquire pixels for idle lanes: one atomic per wave per round
+    for (;;) {
+      const bool need = (w < 0) && !done;
+      const unsigned long long mask = __ballot(need);
+      if (!mask) break;
+      const int leader = __ffsll((long long)mask) - 1;
+      unsigned long long base = 0;
+      if (lane == leader) base = atomicAdd(A.counter, (unsigned long long)__popcll(mask));
+      base = __shfl(base, leader);
+      if (need) {
+        const long long wi = (long long)(base + __popcll(mask & lanes_below));
+        if (wi >= A.work_total) {
+          done = true;
+        } else if (work_pixel(A, wi, px, row)) {
+          w = wi;
+          s = 0;
+          sum = v3(0, 0, 0);
+          path = false;
+        }
+      }
+    }
+    if (w < 0) break;  // no pixel left for this lane (done); the others keep going
+    if (!path) {  // start sample s: uniformRandomUVs' pair, then getRay
+      const uint32_t pid = (uint32_t)((long long)row * A.W + px);
+      g.init(A.seed, pid, (uint32_t)s);
+      const double ru = g.draw(), rv = g.draw();
+      const int y = A.H - 1 - row;
+      const double u = ((double)px + ru) / (double)A.W;
+      const double v = ((double)y + rv) / (double)A.H;
+      ray = get_ray(A.cam, u, v, g);
+      thr = v3(1.0, 1.0, 1.0);
+      depth = A.max_depth;
+      path = true;
+    }
+    V3 contrib;
+    if (segment<F>(A, ray, thr, depth, g, stk, contrib)) {
+      sum = sum + contrib;
+      path = false;
+      ++s;
+      const bool all_nan = (A.flags & RT_FLAG_NAN_CULL) && sum.x != sum.x && sum.y != sum.y && sum.z != sum.z;
+      if (s == A.spp || all_nan) {
+        store_pixel(A, w, divide(sum, (double)A.spp));
+        w = -1;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- tier A: the reference's stream
+// One lane per image column; rows top to bottom; each pixel draws its 2*ns UVs first and uses
+// them in reverse draw order (uniformRandomUVs' foldr, Lib.hs:1358-1371) — the UV pairs are
+// recomputed from the pixel's starting state (SplitMix is seed + k*gamma), no list is stored.
+template <unsigned F>
+__global__ void __launch_bounds__(RT_BLOCK) render_exact(RenderArgs A) {
+  __shared__ int stk_mem[RT_STACK * RT_BLOCK];
+  int* stk = &stk_mem[threadIdx.x];
+  const int x = blockIdx.x * RT_BLOCK + threadIdx.x;
+  if (x >= A.W) return;
+  RngExact g{A.gens[2 * x], A.gens[2 * x + 1]};
+  const int ns = A.spp;
+  for (int row = 0; row < A.H; ++row) {
+    const int y = A.H - 1 - row;
+    const uint64_t seed0 = g.seed;
+    g.seed += (uint64_t)(2 * (long long)ns) * g.gamma;
+    V3 sum = v3(0, 0, 0);
+    for (int j = 0; j < ns; ++j) {
+      const int i = ns - 1 - j;
+      const double ru = word_to_draw(mix64(seed0 + (uint64_t)(2 * i + 1) * g.gamma));
+      const double rv = word_to_draw(mix64(seed0 + (uint64_t)(2 * i + 2) * g.gamma));
+      const double u = ((double)x + ru) / (double)A.W;
+      const double v = ((double)y + rv) / (double)A.H;
+      Ray ray = get_ray(A.cam, u, v, g);
+      V3 thr = v3(1.0, 1.0, 1.0), contrib;
+      int depth = A.max_depth;
+      while (!segment<F>(A, ray, thr, depth, g, stk, contrib)) {
+      }
+      sum = sum + contrib;
+    }
+    store_pixel(A, (long long)row * A.W + x, divide(sum, (double)ns));
+  }
+  A.gens[2 * x] = g.seed;
+}
+
+// ---------------------------------------------------------------- slab -> image
+template <class T>
+__global__ void assemble(const T* slabs, T* image, int W, int H, int tile, int tiles_x, int shards,
+                         long long slab_pixels) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)W * H) return;
+  const int row = (int)(i / W), px = (int)(i % W);
+  const int gt = (row / tile) * tiles_x + (px / tile);
+  const int shard = gt % shards;
+  const long long lt = gt / shards;
+  const int bpr = tile >> 3;
+  const int bx = (px % tile) >> 3, by = (row % tile) >> 3;
+  const int within = (by * bpr + bx) * 64 + (row & 7) * 8 + (px & 7);
+  const long long src = (long long)shard * slab_pixels + lt * tile * tile + within;
+  image[i * 3 + 0] = slabs[src * 3 + 0];
+  image[i * 3 + 1] = slabs[src * 3 + 1];
+  image[i * 3 + 2] = slabs[src * 3 + 2];
+}
+
+// ---------------------------------------------------------------- debug: closest hits
+__global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* rays, int n, double tmin,
+                                                         double tmax, uint64_t seed, double* out) {
+  __shared__ int stk_mem[RT_STACK * RT_BLOCK];
+  int* stk = &stk_mem[threadIdx.x];
+  const int i = blockIdx.x * RT_BLOCK + threadIdx.x;
+  if (i >= n) return;
+  const double* q = rays + 7 * (long long)i;
+  const Ray r{v3(q[0], q[1], q[2]), v3(q[3], q[4], q[5]), q[6]};
+  RngPhilox g;
+  g.init(seed, (uint32_t)i, 0);
+  Hit h;
+  double* o = out + 12 * (long long)i;
+  if (traverse<F_ALL>(S, S.world, r, tmin, tmax, h, g, stk)) {
+    o[0] = 1; o[1] = h.t;
+    o[2] = h.p.x; o[3] = h.p.y; o[4] = h.p.z;
+    o[5] = h.n.x; o[6] = h.n.y; o[7] = h.n.z;
+    o[8] = h.u; o[9] = h.v; o[10] = h.ff; o[11] = h.mat;
+  } else {
+    for (int k = 0; k < 12; ++k) o[k] = 0;
+  }
+}
+
+}  // namespace
+
+// =================================================================== host side
+struct rt_ctx {
+  int device = 0;
+  int cu_count = 0;
+  int blocks_per_cu = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // device scene
+  rt_node* d_nodes = nullptr;
+  DMat* d_mats = nullptr;
+  rt_texture* d_texs = nullptr;
+  rt_perlin* d_perlins = nullptr;
+  rt_image* d_images = nullptr;
+  uint8_t* d_pool = nullptr;
+  Scene scene{};
+  unsigned features = 0;
+  bool has_scene = false;
+  unsigned long long* d_counter = nullptr;
+  double last_ms = 0.0;
+};
+
+namespace {
+
+int hip_fail(hipError_t e, const char* what) {
+  rt::set_error(std::string(what) + ": " + hipGetErrorString(e));
+  return RT_E_HIP;
+}
+#define HIPCHK(x)                                  \
+  do {                                             \
+    hipError_t _e = (x);                           \
+    if (_e != hipSuccess) return hip_fail(_e, #x); \
+  } while (0)
+
+int invalid(const std::string& s) {
+  rt::set_error(s);
+  return RT_E_INVALID;
+}
+int unsupported(const std::string& s) {
+  rt::set_error(s);
+  return RT_E_UNSUPPORTED;
+}
+
+void free_scene(rt_ctx* c) {
+  (void)hipFree(c->d_nodes);
+  (void)hipFree(c->d_mats);
+  (void)hipFree(c->d_texs);
+  (void)hipFree(c->d_perlins);
+  (void)hipFree(c->d_images);
+  (void)hipFree(c->d_pool);
+  c->d_nodes = nullptr;
+  c->d_mats = nullptr;
+  c->d_texs = nullptr;
+  c->d_perlins = nullptr;
+  c->d_images = nullptr;
+  c->d_pool = nullptr;
+  c->has_scene = false;
+}
+
+bool is_leaf_prim(int type) {
+  return type == RT_NODE_SPHERE || type == RT_NODE_MOVING_SPHERE || type == RT_NODE_CUBOID ||
+         (type >= RT_NODE_RECT_XY && type <= RT_NODE_RECT_YZ);
+}
+
+struct Validator {
+  const rt_scene_desc* d;
+  std::vector<rt_node> nodes;  // device copy (type flags added)
+  std::vector<int> stack_need, chain_prim;
+  std::string err;
+
+  bool child_ok(int parent, int child) { return child >= 0 && child < parent; }
+
+  bool run() {
+    const int n = d->n_nodes;
+    if (n <= 0 || !d->nodes) return fail("scene has no nodes");
+    nodes.assign(d->nodes, d->nodes + n);
+    stack_need.assign(n, 0);
+    chain_prim.assign(n, 0);
+    for (int i = 0; i < n; ++i) {
+      rt_node& x = nodes[i];
+      const int t = x.type;
+      switch (t) {
+        case RT_NODE_BVH:
+          if (!child_ok(i, x.a) || !child_ok(i, x.b)) return fail("BVH child must precede its parent");
+          if (x.c <= 0) return fail("BVH size must be positive");
+          stack_need[i] = std::max(1 + stack_need[x.a], stack_need[x.b]);
+          break;
+        case RT_NODE_SPHERE:
+        case RT_NODE_RECT_XY:
+        case RT_NODE_RECT_XZ:
+        case RT_NODE_RECT_YZ:
+        case RT_NODE_CUBOID:
+          if (x.a < 0 || x.a >= d->n_materials) return fail("primitive material out of range");
+          chain_prim[i] = 1;
+          break;
+        case RT_NODE_MOVING_SPHERE:
+          if (x.a < 0 || x.a >= d->n_materials) return fail("primitive material out of range");
+          if (i + 1 >= n || d->nodes[i + 1].type != RT_NODE_EXT) return fail("MovingSphere needs its EXT record");
+          chain_prim[i] = 1;
+          break;
+        case RT_NODE_TRANSLATE:
+        case RT_NODE_ROTATE:
+          if (!child_ok(i, x.a)) return fail("instance child must precede its parent");
+          if (t == RT_NODE_ROTATE && (x.b < 0 || x.b > 2)) return fail("rotate axis out of range");
+          if (chain_prim[x.a]) {
+            chain_prim[i] = 1;
+            x.type |= RT_CHAIN_PRIM;
+          } else {
+            stack_need[i] = 1 + stack_need[x.a];
+          }
+          break;
+        case RT_NODE_CONSTANT_MEDIUM:
+          if (!child_ok(i, x.a)) return fail("medium boundary must precede the medium");
+          if (!chain_prim[x.a])
+            return unsup("ConstantMedium boundary must be a primitive or a Translate/Rotate chain of one");
+          if (x.b < 0 || x.b >= d->n_materials) return fail("medium material out of range");
+          break;
+        case RT_NODE_UNHITTABLE:
+        case RT_NODE_EXT:
+          break;
+        default:
+          return fail("unknown node type");
+      }
+    }
+    if (d->world_root < 0 || d->world_root >= n) return fail("world root out of range");
+    if (stack_need[d->world_root] > RT_STACK - 2) return unsup("scene BVH too deep for the LDS traversal stack");
+    if (d->lights_root >= n) return fail("lights root out of range");
+    if (d->lights_root >= 0 && !check_lights(d->lights_root, 0)) return false;
+    return true;
+  }
+  bool has_media(int id) {
+    const rt_node& x = d->nodes[id];
+    if (x.type == RT_NODE_CONSTANT_MEDIUM) return true;
+    if (x.type == RT_NODE_BVH) return has_media(x.a) || has_media(x.b);
+    if (x.type == RT_NODE_TRANSLATE || x.type == RT_NODE_ROTATE) return has_media(x.a);
+    return false;
+  }
+  bool check_lights(int id, int depth) {
+    if (has_media(id)) return unsup("lights tree must not contain ConstantMedium");
+    if (stack_need[id] > RT_STACK - 2) return unsup("lights tree too deep");
+    const rt_node& x = d->nodes[id];
+    if (x.type == RT_NODE_BVH) {
+      if (depth >= RT_LIGHT_DEPTH) return unsup("lights BVH deeper than RT_LIGHT_DEPTH");
+      return check_lights(x.a, depth + 1) && check_lights(x.b, depth + 1);
+    }
+    return true;
+  }
+  bool fail(const char* m) {
+    err = m;
+    code = RT_E_INVALID;
+    return false;
+  }
+  bool unsup(const char* m) {
+    err = m;
+    code = RT_E_UNSUPPORTED;
+    return false;
+  }
+  int code = RT_OK;
+};
+
+bool tex_needs_uv(const rt_scene_desc* d, int tid, int guard = 0) {
+  if (tid < 0 || tid >= d->n_textures || guard > 64) return false;
+  const rt_texture& t = d->textures[tid];
+  if (t.type == RT_TEX_IMAGE) return true;
+  if (t.type == RT_TEX_CHECKER) return tex_needs_uv(d, t.a, guard + 1) || tex_needs_uv(d, t.b, guard + 1);
+  return false;
+}
+
+template <class T>
+int upload(T** dst, const T* src, size_t count) {
+  if (count == 0 || !src) return RT_OK;
+  HIPCHK(hipMalloc((void**)dst, sizeof(T) * count));
+  HIPCHK(hipMemcpy(*dst, src, sizeof(T) * count, hipMemcpyHostToDevice));
+  return RT_OK;
+}
+
+int check_params(const rt_render_params* p) {
+  if (!p) return invalid("null params");
+  if (p->width <= 0 || p->height <= 0 || p->spp <= 0 || p->max_depth < 0)
+    return invalid("width/height/spp must be positive and max_depth >= 0");
+  if (p->rng_mode != RT_RNG_EXACT && p->rng_mode != RT_RNG_PHILOX) return invalid("unknown rng_mode");
+  const int tile = p->tile ? p->tile : 16;
+  if (tile <= 0 || tile % 8) return invalid("tile must be a positive multiple of 8");
+  if (p->shard_count < 0 || (p->shard_count > 0 && (p->shard_rank < 0 || p->shard_rank >= p->shard_count)))
+    return invalid("bad shard_rank/shard_count");
+  if ((long long)p->width * p->height >= (1ll << 32)) return invalid("image too large for 32-bit pixel ids");
+  return RT_OK;
+}
+
+void geometry(const rt_render_params* p, int& tile, int& tiles_x, long long& tiles_total, long long& per_shard,
+              long long& slab_pixels) {
+  tile = p->tile ? p->tile : 16;
+  const int shards = p->shard_count > 0 ? p->shard_count : 1;
+  tiles_x = (p->width + tile - 1) / tile;
+  const int tiles_y = (p->height + tile - 1) / tile;
+  tiles_total = (long long)tiles_x * tiles_y;
+  per_shard = (tiles_total + shards - 1) / shards;
+  slab_pixels = per_shard * tile * tile;
+}
+
+// Kernel variants: spheres-only (configs 1, 2, 5), Cornell-like (rects, instances, lights), full.
+constexpr unsigned kVarSpheres = 0u;
+constexpr unsigned kVarCornell = F_RECT | F_INST | F_LIGHTS;
+unsigned variant_for(unsigned f) {
+  if ((f & ~kVarSpheres) == 0) return kVarSpheres;
+  if ((f & ~kVarCornell) == 0) return kVarCornell;
+  return F_ALL;
+}
+const void* philox_variant(unsigned f) {
+  switch (variant_for(f)) {
+    case kVarSpheres: return (const void*)render_philox<kVarSpheres>;
+    case kVarCornell: return (const void*)render_philox<kVarCornell>;
+    default: return (const void*)render_philox<F_ALL>;
+  }
+}
+const void* exact_variant(unsigned f) {
+  switch (variant_for(f)) {
+    case kVarSpheres: return (const void*)render_exact<kVarSpheres>;
+    case kVarCornell: return (const void*)render_exact<kVarCornell>;
+    default: return (const void*)render_exact<F_ALL>;
+  }
+}
+
+unsigned scene_features(const rt_scene_desc* d) {
+  unsigned f = 0;
+  for (int i = 0; i < d->n_nodes; ++i) {
+    switch (d->nodes[i].type) {
+      case RT_NODE_BVH:
+      case RT_NODE_SPHERE: break;
+      case RT_NODE_MOVING_SPHERE: f |= F_MOVING; break;
+      case RT_NODE_TRANSLATE:
+      case RT_NODE_ROTATE: f |= F_INST; break;
+      case RT_NODE_CONSTANT_MEDIUM: f |= F_MEDIA; break;
+      default: f |= F_RECT; break;  // rects, cuboids, and anything needing the full dispatch
+    }
+  }
+  if (d->world_root >= 0 && d->world_root < d->n_nodes && d->nodes[d->world_root].type == RT_NODE_UNHITTABLE)
+    f |= F_RECT;
+  if (d->lights_root >= 0) f |= F_LIGHTS;
+  for (int i = 0; i < d->n_textures; ++i)
+    if (d->textures[i].type != RT_TEX_CONSTANT) f |= F_TEX;
+  return f;
+}
+
+int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int rank, int shards, uint8_t* d_rgb,
+                  double* d_lin, hipStream_t st) {
+  RenderArgs A{};
+  A.S = c->scene;
+  A.cam = *cam;
+  A.W = p->width;
+  A.H = p->height;
+  A.spp = p->spp;
+  A.max_depth = p->max_depth;
+  A.flags = p->flags;
+  long long tiles_total, per_shard, slab;
+  geometry(p, A.tile, A.tiles_x, tiles_total, per_shard, slab);
+  A.tiles_total = (int)tiles_total;
+  A.shard_rank = rank;
+  A.shard_count = shards;
+  A.work_total = slab;
+  A.seed = p->seed;
+  A.counter = c->d_counter;
+  A.out_rgb = d_rgb;
+  A.out_lin = d_lin;
+  HIPCHK(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned long long), st));
+  const void* fn = philox_variant(c->features);
+  int bpc = 1;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, RT_BLOCK, 0));
+  const long long want = (slab + RT_BLOCK - 1) / RT_BLOCK;
+  const long long resident = (long long)c->cu_count * std::max(1, bpc);
+  const int grid = (int)std::max(1ll, std::min(want, resident));
+  HIPCHK(hipEventRecord(c->ev0, st));
+  void* args[] = {&A};
+  HIPCHK(hipLaunchKernel(fn, dim3(grid), dim3(RT_BLOCK), args, 0, st));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev1, st));
+  return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_device_count(int* out) {
+  if (!out) return invalid("null out");
+  HIPCHK(hipGetDeviceCount(out));
+  return RT_OK;
+}
+
+int rt_create(int device, rt_ctx** out) {
+  if (!out) return invalid("null out");
+  int n = 0;
+  HIPCHK(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return invalid("device index out of range");
+  HIPCHK(hipSetDevice(device));
+  rt_ctx* c = new rt_ctx();
+  c->device = device;
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, device));
+  c->cu_count = prop.multiProcessorCount;
+  int bpc = 0;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, render_philox<F_ALL>, RT_BLOCK, 0));
+  c->blocks_per_cu = bpc;
+  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIPCHK(hipEventCreate(&c->ev0));
+  HIPCHK(hipEventCreate(&c->ev1));
+  HIPCHK(hipMalloc((void**)&c->d_counter, 256));
+  *out = c;
+  return RT_OK;
+}
+
+void rt_destroy(rt_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  free_scene(c);
+  (void)hipFree(c->d_counter);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int rt_upload_scene(rt_ctx* c, const rt_scene_desc* d) {
+  if (!c || !d) return invalid("null argument");
+  HIPCHK(hipSetDevice(c->device));
+  Validator v{d};
+  if (!v.run()) {
+    rt::set_error("rt_upload_scene: " + v.err);
+    return v.code;
+  }
+  for (int i = 0; i < d->n_textures; ++i) {
+    const rt_texture& t = d->textures[i];
+    if (t.type == RT_TEX_CHECKER && (t.a < 0 || t.a >= i || t.b < 0 || t.b >= i))
+      return invalid("rt_upload_scene: checker children must precede the checker");
+    if (t.type == RT_TEX_PERLIN && (t.a < 0 || t.a >= d->n_perlins)) return invalid("rt_upload_scene: bad perlin id");
+    if (t.type == RT_TEX_IMAGE && t.a >= 0) {
+      if (t.a >= d->n_images) return invalid("rt_upload_scene: bad image id");
+      const rt_image& im = d->images[t.a];
+      if (im.width != t.b || im.height != t.c || im.offset < 0 ||
+          im.offset + (int64_t)im.width * im.height * 3 > d->image_pool_bytes)
+        return invalid("rt_upload_scene: image raster out of the pool");
+    }
+  }
+  std::vector<DMat> mats(d->n_materials);
+  for (int i = 0; i < d->n_materials; ++i) {
+    const rt_material& m = d->materials[i];
+    if (m.type < RT_MAT_LAMBERTIAN || m.type > RT_MAT_ISOTROPIC) return invalid("rt_upload_scene: bad material");
+    if (m.type != RT_MAT_DIELECTRIC && (m.texture < 0 || m.texture >= d->n_textures))
+      return invalid("rt_upload_scene: material texture out of range");
+    mats[i] = DMat{m.type, m.texture, m.param, m.type != RT_MAT_DIELECTRIC && tex_needs_uv(d, m.texture), 0};
+  }
+  free_scene(c);
+  int rc;
+  if ((rc = upload(&c->d_nodes, v.nodes.data(), v.nodes.size())) ||
+      (rc = upload(&c->d_mats, mats.data(), mats.size())) ||
+      (rc = upload(&c->d_texs, d->textures, (size_t)d->n_textures)) ||
+      (rc = upload(&c->d_perlins, d->perlins, (size_t)d->n_perlins)) ||
+      (rc = upload(&c->d_images, d->images, (size_t)d->n_images)) ||
+      (rc = upload(&c->d_pool, d->image_pool, (size_t)d->image_pool_bytes))) {
+    free_scene(c);
+    return rc;
+  }
+  Scene& S = c->scene;
+  S.nodes = c->d_nodes;
+  S.mats = c->d_mats;
+  S.texs = c->d_texs;
+  S.perlins = c->d_perlins;
+  S.images = c->d_images;
+  S.pool = c->d_pool;
+  S.world = d->world_root;
+  S.lights = d->lights_root;
+  for (int i = 0; i < 3; ++i) S.bg[i] = d->background[i];
+  c->features = scene_features(d);
+  c->has_scene = true;
+  return RT_OK;
+}
+
+int rt_shard_geometry(const rt_render_params* p, int64_t* tiles_total, int64_t* tiles_per_shard,
+                      int64_t* slab_pixels) {
+  int rc = check_params(p);
+  if (rc) return rc;
+  int tile, tiles_x;
+  long long tt, ps, sp;
+  geometry(p, tile, tiles_x, tt, ps, sp);
+  if (tiles_total) *tiles_total = tt;
+  if (tiles_per_shard) *tiles_per_shard = ps;
+  if (slab_pixels) *slab_pixels = sp;
+  return RT_OK;
+}
+
+int rt_render_shard_async(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, uint8_t* d_rgb, double* d_lin,
+                          void* stream) {
+  if (!c || !cam || !d_rgb) return invalid("null argument");
+  int rc = check_params(p);
+  if (rc) return rc;
+  if (!c->has_scene) {
+    rt::set_error("rt_render_shard_async: no scene uploaded");
+    return RT_E_STATE;
+  }
+  if (p->rng_mode != RT_RNG_PHILOX) return invalid("sharded rendering needs RT_RNG_PHILOX (tier B)");
+  HIPCHK(hipSetDevice(c->device));
+  const int shards = p->shard_count > 0 ? p->shard_count : 1;
+  return launch_philox(c, cam, p, p->shard_rank, shards, d_rgb, d_lin, (hipStream_t)stream);
+}
+
+int rt_assemble_async(rt_ctx* c, const rt_render_params* p, const uint8_t* d_slabs, uint8_t* d_image, void* stream) {
+  if (!c || !d_slabs || !d_image) return invalid("null argument");
+  int rc = check_params(p);
+  if (rc) return rc;
+  int tile, tiles_x;
+  long long tt, ps, sp;
+  geometry(p, tile, tiles_x, tt, ps, sp);
+  const long long n = (long long)p->width * p->height;
+  hipLaunchKernelGGL(assemble<uint8_t>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_slabs,
+                     d_image, p->width, p->height, tile, tiles_x, p->shard_count > 0 ? p->shard_count : 1, sp);
+  HIPCHK(hipGetLastError());
+  return RT_OK;
+}
+
+int rt_assemble_linear_async(rt_ctx* c, const rt_render_params* p, const double* d_slabs, double* d_image,
+                             void* stream) {
+  if (!c || !d_slabs || !d_image) return invalid("null argument");
+  int rc = check_params(p);
+  if (rc) return rc;
+  int tile, tiles_x;
+  long long tt, ps, sp;
+  geometry(p, tile, tiles_x, tt, ps, sp);
+  const long long n = (long long)p->width * p->height;
+  hipLaunchKernelGGL(assemble<double>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_slabs,
+                     d_image, p->width, p->height, tile, tiles_x, p->shard_count > 0 ? p->shard_count : 1, sp);
+  HIPCHK(hipGetLastError());
+  return RT_OK;
+}
+
+int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, const uint64_t* col_gens, uint8_t* out_rgb,
+              double* out_lin, uint64_t* out_gens) {
+  if (!c || !cam || !pin || !out_rgb) return invalid("null argument");
+  int rc = check_params(pin);
+  if (rc) return rc;
+  if (!c->has_scene) {
+    rt::set_error("rt_render: no scene uploaded");
+    return RT_E_STATE;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  rt_render_params p = *pin;
+  p.shard_rank = 0;
+  p.shard_count = 1;
+  const long long npx = (long long)p.width * p.height;
+  hipStream_t st = c->stream;
+  uint8_t* d_img = nullptr;
+  double* d_img_lin = nullptr;
+  HIPCHK(hipMalloc((void**)&d_img, (size_t)npx * 3));
+  if (out_lin) HIPCHK(hipMalloc((void**)&d_img_lin, sizeof(double) * (size_t)npx * 3));
+  int result = RT_OK;
+  if (p.rng_mode == RT_RNG_PHILOX) {
+    int tile, tiles_x;
+    long long tt, ps, slab;
+    geometry(&p, tile, tiles_x, tt, ps, slab);
+    uint8_t* d_slab = nullptr;
+    double* d_slab_lin = nullptr;
+    HIPCHK(hipMalloc((void**)&d_slab, (size_t)slab * 3));
+    if (out_lin) HIPCHK(hipMalloc((void**)&d_slab_lin, sizeof(double) * (size_t)slab * 3));
+    result = launch_philox(c, cam, &p, 0, 1, d_slab, d_slab_lin, st);
+    if (!result) result = rt_assemble_async(c, &p, d_slab, d_img, st);
+    if (!result && out_lin) result = rt_assemble_linear_async(c, &p, d_slab_lin, d_img_lin, st);
+    HIPCHK(hipStreamSynchronize(st));
+    (void)hipFree(d_slab);
+    (void)hipFree(d_slab_lin);
+  } else {
+    if (!col_gens) return invalid("rt_render: tier A needs col_gens (2*width words)");
+    uint64_t* d_gens = nullptr;
+    HIPCHK(hipMalloc((void**)&d_gens, sizeof(uint64_t) * 2 * (size_t)p.width));
+    HIPCHK(hipMemcpyAsync(d_gens, col_gens, sizeof(uint64_t) * 2 * (size_t)p.width, hipMemcpyHostToDevice, st));
+    RenderArgs A{};
+    A.S = c->scene;
+    A.cam = *cam;
+    A.W = p.width;
+    A.H = p.height;
+    A.spp = p.spp;
+    A.max_depth = p.max_depth;
+    A.gens = d_gens;
+    A.out_rgb = d_img;
+    A.out_lin = d_img_lin;
+    HIPCHK(hipEventRecord(c->ev0, st));
+    void* args[] = {&A};
+    HIPCHK(hipLaunchKernel(exact_variant(c->features), dim3((p.width + RT_BLOCK - 1) / RT_BLOCK), dim3(RT_BLOCK),
+                           args, 0, st));
+    HIPCHK(hipEventRecord(c->ev1, st));
+    if (out_gens)
+      HIPCHK(hipMemcpyAsync(out_gens, d_gens, sizeof(uint64_t) * 2 * (size_t)p.width, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    (void)hipFree(d_gens);
+  }
+  if (result) return result;
+  HIPCHK(hipMemcpy(out_rgb, d_img, (size_t)npx * 3, hipMemcpyDeviceToHost));
+  if (out_lin) HIPCHK(hipMemcpy(out_lin, d_img_lin, sizeof(double) * (size_t)npx * 3, hipMemcpyDeviceToHost));
+  (void)hipFree(d_img);
+  (void)hipFree(d_img_lin);
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  c->last_ms = ms;
+  return RT_OK;
+}
+
+int rt_last_kernel_ms(rt_ctx* c, double* out_ms) {
+  if (!c || !out_ms) return invalid("null argument");
+  float ms = 0;
+  HIPCHK(hipEventSynchronize(c->ev1));
+  HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  c->last_ms = ms;
+  *out_ms = ms;
+  return RT_OK;
+}
+
+int rt_debug_closest_hits(rt_ctx* c, const double* rays, int n, double tmin, double tmax, uint64_t seed, double* out) {
+  if (!c || !rays || !out || n < 0) return invalid("null argument");
+  if (!c->has_scene) {
+    rt::set_error("rt_debug_closest_hits: no scene uploaded");
+    return RT_E_STATE;
+  }
+  if (n == 0) return RT_OK;
+  HIPCHK(hipSetDevice(c->device));
+  double *d_rays = nullptr, *d_out = nullptr;
+  HIPCHK(hipMalloc((void**)&d_rays, sizeof(double) * 7 * (size_t)n));
+  HIPCHK(hipMalloc((void**)&d_out, sizeof(double) * 12 * (size_t)n));
+  HIPCHK(hipMemcpy(d_rays, rays, sizeof(double) * 7 * (size_t)n, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(closest_hits, dim3((n + RT_BLOCK - 1) / RT_BLOCK), dim3(RT_BLOCK), 0, c->stream, c->scene,
+                     d_rays, n, tmin, tmax, seed, d_out);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpy(out, d_out, sizeof(double) * 12 * (size_t)n, hipMemcpyDeviceToHost));
+  (void)hipFree(d_rays);
+  (void)hipFree(d_out);
+  return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,467 @@
+// rt_trace.h — intersection, traversal, light sampling, textures and scattering (device).
+#pragma once
+#include "rt_device.h"
+
+namespace rtd {
+
+// Scene features a kernel variant is compiled for (host picks the variant per scene).
+enum : unsigned {
+  F_RECT = 1u,    // Rect / Cuboid nodes
+  F_MOVING = 2u,  // MovingSphere
+  F_INST = 4u,    // Translate / Rotate
+  F_MEDIA = 8u,   // ConstantMedium (+ Isotropic)
+  F_LIGHTS = 16u, // a lights tree (Lambertian light sampling / pdf)
+  F_TEX = 32u,    // Checker / Perlin / Image textures (and sphere u, v)
+  F_ALL = 63u
+};
+
+// ------------------------------------------------------------------ textures (Lib.hs:441-513)
+__device__ __forceinline__ int hmod256(long long a) {  // Haskell `mod` pointCount
+  const long long r = a % 256;
+  return (int)(r < 0 ? r + 256 : r);
+}
+__device__ inline double noise(const rt_perlin* P, double sc, V3 p) {  // Lib.hs:441-461
+  const V3 q = scale(sc, p);
+  const double fi = floor(q.x), fj = floor(q.y), fk = floor(q.z);
+  const long long i = (long long)fi, j = (long long)fj, k = (long long)fk;
+  const double u = q.x - (double)i, v = q.y - (double)j, w = q.z - (double)k;
+  const double uu = u * u * (3 - 2 * u), vv = v * v * (3 - 2 * v), ww = w * w * (3 - 2 * w);
+  double acc = 0.0;
+  // perlinInterp's foldr: corner (1,1,1) is added first, (0,0,0) last (Lib.hs:477-484)
+#pragma unroll
+  for (int idx = 7; idx >= 0; --idx) {
+    const int di = (idx >> 2) & 1, dj = (idx >> 1) & 1, dk = idx & 1;
+    const int r = P->perm_x[hmod256(i + di)] ^ P->perm_y[hmod256(j + dj)] ^ P->perm_z[hmod256(k + dk)];
+    const V3 val = vload(P->ranvec[r]);
+    const double I = di, J = dj, K = dk;
+    acc = acc + ((I * uu + (1 - I) * (1 - uu)) * (J * vv + (1 - J) * (1 - vv)) * (K * ww + (1 - K) * (1 - ww)) *
+                 dot(val, v3(u - I, v - J, w - K)));
+  }
+  return acc;
+}
+__device__ inline double turb(const rt_perlin* P, double sc, V3 p) {  // Lib.hs:486-494, depth 7
+  double acc = 0.0, weight = 1.0;
+  V3 tp = p;
+  for (int d = 0; d < 7; ++d) {
+    acc = acc + weight * noise(P, sc, tp);
+    tp = scale(2.0, tp);
+    weight = weight * 0.5;
+  }
+  return fabs(acc);
+}
+// textureValue (Lib.hs:496-510); checker chains are followed iteratively.
+template <unsigned F>
+__device__ inline V3 texture_value(const Scene& S, int tid, double u, double v, V3 p) {
+  const rt_texture* t = &S.texs[tid];
+  if constexpr (!(F & F_TEX)) return v3(t->f[0], t->f[1], t->f[2]);
+  while (t->type == RT_TEX_CHECKER) {
+    const bool odd = sin(10 * p.x) * sin(10 * p.y) * sin(10 * p.z) < 0;
+    t = &S.texs[odd ? t->a : t->b];
+  }
+  if (t->type == RT_TEX_CONSTANT) return v3(t->f[0], t->f[1], t->f[2]);
+  if (t->type == RT_TEX_PERLIN) {
+    const double m = 0.5 * (1.0 + sin(p.z + 10 * turb(&S.perlins[t->a], t->f[0], p)));  // marbleTexture
+    return scale(m, v3(1.0, 1.0, 1.0));
+  }
+  // RT_TEX_IMAGE
+  if (t->a < 0) return v3(0, 1, 1);
+  const rt_image im = S.images[t->a];
+  const double nxd = (double)t->b;
+  double ci = u * nxd;
+  ci = ci < 0 ? 0 : (ci > nxd - kEps ? nxd - kEps : ci);
+  const double nyd = (double)t->c;
+  double cj = (1.0 - v) * nyd - kEps;
+  cj = cj < 0 ? 0 : (cj > nyd - kEps ? nyd - kEps : cj);
+  const int i = ci == ci ? (int)floor(ci) : 0, j = cj == cj ? (int)floor(cj) : 0;
+  const uint8_t* px = S.pool + im.offset + ((long long)j * im.width + i) * 3;
+  return v3(px[0] / 255.0, px[1] / 255.0, px[2] / 255.0);  // colorToAlbedo (Lib.hs:294-297)
+}
+
+// ------------------------------------------------------------------ primitives
+// boxRayIntersect (Lib.hs:798-814): per-axis slab with true division, GHC max/min.
+__device__ __forceinline__ bool box_hit(const double* f, const Ray& r, double t_min, double t_max) {
+  bool ok = true;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const double o = comp(r.o, a), d = comp(r.d, a);
+    const double ta = (f[a] - o) / d;
+    const double tb = (f[a + 3] - o) / d;
+    const bool lt = ta < tb;
+    const double t0 = lt ? ta : tb, t1 = lt ? tb : ta;
+    const double lo = gmax(t0, t_min);
+    const double hi = gmin(t1, t_max);
+    ok = ok && (hi > lo);
+  }
+  return ok;
+}
+
+// rectHit (Lib.hs:1005-1028); plane 0 XY, 1 XZ, 2 YZ. Rejects only t < tmin or t > tmax.
+__device__ __forceinline__ bool rect_hit(int plane, double i0, double i1, double j0, double j1, double k, int mat,
+                                         const Ray& r, double t_min, double t_max, Hit& h) {
+  const int ii = plane == 2 ? 1 : 0, jj = plane == 0 ? 1 : 2, kk = plane == 0 ? 2 : (plane == 1 ? 1 : 0);
+  const double t = (k - comp(r.o, kk)) / comp(r.d, kk);
+  if ((t < t_min) || (t > t_max)) return false;
+  const double i = comp(r.o, ii) + t * comp(r.d, ii);
+  const double j = comp(r.o, jj) + t * comp(r.d, jj);
+  if ((i < i0) || (i > i1) || (j < j0) || (j > j1)) return false;
+  h.t = t;
+  h.u = (i - i0) / (i1 - i0);
+  h.v = (j - j0) / (j1 - j0);
+  h.p = at(r, t);
+  const V3 outward = plane == 0 ? v3(0, 0, 1) : (plane == 1 ? v3(0, 1, 0) : v3(1, 0, 0));
+  face_normal(r, outward, h.ff, h.n);
+  h.mat = mat;
+  return true;
+}
+
+// hit Sphere (Lib.hs:1081-1105): strict tmin < t < tmax.
+template <unsigned F>
+__device__ __forceinline__ bool sphere_hit(const Scene& S, V3 sc, double sr, int sm, const Ray& r, double t_min,
+                                           double t_max, Hit& h) {
+  const V3 oc = r.o - sc;
+  const double a = dot(r.d, r.d);
+  const double b = dot(oc, r.d);
+  const double c = dot(oc, oc) - (sr * sr);
+  const double disc = b * b - a * c;
+  if (!(disc > 0)) return false;
+  const double sd = sqrt(disc);
+  const double temp1 = ((-b) - sd) / a;
+  const double temp2 = ((-b) + sd) / a;
+  double temp;
+  if (t_min < temp1 && temp1 < t_max) temp = temp1;
+  else if (t_min < temp2 && temp2 < t_max) temp = temp2;
+  else return false;
+  h.t = temp;
+  h.p = at(r, temp);
+  const V3 outward = divide(h.p - sc, sr);
+  face_normal(r, outward, h.ff, h.n);
+  h.mat = sm;
+  if ((F & F_TEX) && S.mats[sm].needs_uv) {  // u, v only feed image textures; skip atan2/asin otherwise
+    const double phi = ghc_atan2(outward.z, outward.x);
+    const double theta = asin(outward.y);
+    h.u = 1.0 - ((phi + kPi) / (2 * kPi));
+    h.v = (theta + (kPi / 2)) / kPi;
+  } else {
+    h.u = 0.0;
+    h.v = 0.0;
+  }
+  return true;
+}
+
+// Leaf primitives: Sphere, MovingSphere, Rect{XY,XZ,YZ}, Cuboid.
+template <unsigned F>
+__device__ inline bool prim_hit(const Scene& S, int id, const Ray& r, double t_min, double t_max, Hit& h) {
+  const rt_node* n = &S.nodes[id];
+  const int type = n->type & RT_TYPE_MASK;
+  if (!(F & (F_RECT | F_MOVING)) || type == RT_NODE_SPHERE)
+    return sphere_hit<F>(S, vload(n->f), n->f[3], n->a, r, t_min, t_max, h);
+  if ((F & F_MOVING) && type == RT_NODE_MOVING_SPHERE) {  // Lib.hs:1106-1108
+    const rt_node* e = n + 1;
+    const V3 c0 = vload(n->f), c1 = vload(n->f + 3);
+    const V3 sc = c0 + scale((r.tm - e->f[0]) / e->f[2], c1 - c0);
+    return sphere_hit<F>(S, sc, e->f[3], n->a, r, t_min, t_max, h);
+  }
+  if constexpr (!(F & F_RECT)) return false;
+  if (type == RT_NODE_CUBOID) {  // Lib.hs:989-1004: foldr closerHit; ties go to the later face
+    const double x0 = n->f[0], y0 = n->f[1], z0 = n->f[2], x1 = n->f[3], y1 = n->f[4], z1 = n->f[5];
+    bool have = false;
+    for (int i = 5; i >= 0; --i) {
+      const int plane = i >> 1;
+      const double a0 = plane == 2 ? y0 : x0, a1 = plane == 2 ? y1 : x1;
+      const double b0 = plane == 0 ? y0 : z0, b1 = plane == 0 ? y1 : z1;
+      const double k = (i & 1) ? (plane == 0 ? z0 : (plane == 1 ? y0 : x0)) : (plane == 0 ? z1 : (plane == 1 ? y1 : x1));
+      Hit hh;
+      if (rect_hit(plane, a0, a1, b0, b1, k, n->a, r, t_min, t_max, hh)) {
+        if (!have || hh.t < h.t) {
+          h = hh;
+          have = true;
+        }
+      }
+    }
+    return have;
+  }
+  if (type >= RT_NODE_RECT_XY && type <= RT_NODE_RECT_YZ)
+    return rect_hit(type - RT_NODE_RECT_XY, n->f[0], n->f[1], n->f[2], n->f[3], n->f[4], n->a, r, t_min, t_max, h);
+  return false;
+}
+
+// One instance transform applied to the ray handed to the child (Lib.hs:1029-1031, 1038-1043).
+__device__ __forceinline__ Ray enter_instance(const rt_node* n, const Ray& r) {
+  if ((n->type & RT_TYPE_MASK) == RT_NODE_TRANSLATE) return Ray{r.o - vload(n->f), r.d, r.tm};
+  const int ax = n->b;
+  return Ray{unrotate_point(ax, n->f[0], n->f[1], r.o), unrotate_point(ax, n->f[0], n->f[1], r.d), r.tm};
+}
+// The instance's rewrite of its child's hit; `rc` is the ray the child saw (Lib.hs:1033-1036, 1046-1052).
+__device__ __forceinline__ void exit_instance(const rt_node* n, const Ray& rc, Hit& h) {
+  if ((n->type & RT_TYPE_MASK) == RT_NODE_TRANSLATE) {
+    face_normal(rc, h.n, h.ff, h.n);
+    h.p = h.p + vload(n->f);
+  } else {
+    const int ax = n->b;
+    h.p = rotate_point(ax, n->f[0], n->f[1], h.p);
+    const V3 rn = rotate_point(ax, n->f[0], n->f[1], h.n);
+    face_normal(rc, rn, h.ff, h.n);
+  }
+}
+
+// A Translate/Rotate chain that ends in a leaf primitive (or the leaf itself), hit as one unit.
+template <unsigned F>
+__device__ inline bool chain_hit(const Scene& S, int id, const Ray& ray, double t_min, double t_max, Hit& h) {
+  if constexpr (!(F & F_INST)) return prim_hit<F>(S, id, ray, t_min, t_max, h);
+  Ray r = ray;
+  int cur = id, depth = 0;
+  while (true) {
+    const int type = S.nodes[cur].type & RT_TYPE_MASK;
+    if (type != RT_NODE_TRANSLATE && type != RT_NODE_ROTATE) break;
+    r = enter_instance(&S.nodes[cur], r);
+    cur = S.nodes[cur].a;
+    ++depth;
+  }
+  if (!prim_hit<F>(S, cur, r, t_min, t_max, h)) return false;
+  for (int lv = depth - 1; lv >= 0; --lv) {  // rewrite from the innermost instance outwards
+    Ray rl = ray;
+    int nd = id;
+    for (int k = 0; k < lv; ++k) {
+      rl = enter_instance(&S.nodes[nd], rl);
+      nd = S.nodes[nd].a;
+    }
+    const Ray rc = enter_instance(&S.nodes[nd], rl);
+    exit_instance(&S.nodes[nd], rc, h);
+  }
+  return true;
+}
+
+// hit ConstantMedium (Lib.hs:1053-1080). The boundary is a primitive chain (host-validated).
+template <unsigned F, class R>
+__device__ inline bool medium_hit(const Scene& S, const rt_node* n, const Ray& r, double t_min, double t_max, R& g,
+                                  Hit& h) {
+  Hit h1, h2;
+  if (!chain_hit<F>(S, n->a, r, -INFINITY, INFINITY, h1)) return false;
+  if (!chain_hit<F>(S, n->a, r, h1.t + kEps, INFINITY, h2)) return false;
+  const double rec1tp = gmax(t_min, h1.t);
+  const double rec2t = gmin(t_max, h2.t);
+  if (rec1tp >= rec2t) return false;
+  const double rec1t = rec1tp < 0 ? 0 : rec1tp;
+  const double ray_length = vlen(r.d);
+  const double dist_inside = (rec2t - rec1t) * ray_length;
+  const double rnd = g.draw();
+  const double hit_dist = n->f[0] * log(rnd);
+  if (hit_dist > dist_inside) return false;
+  const double newt = rec1t + (hit_dist / ray_length);
+  h.t = newt;
+  h.p = at(r, newt);
+  h.n = v3(1, 0, 0);
+  h.u = 0;
+  h.v = 0;
+  h.ff = 1;
+  h.mat = n->b;
+  return true;
+}
+
+// ------------------------------------------------------------------ traversal
+// Closest hit over the DAG rooted at `root` in [t_min, t_max] (hit, Lib.hs:970-1109).
+// Depth-first, left child first, each visit bounded by the closest hit so far: exactly the
+// reference's recursion (including media draw order). Instances whose subtree is not a plain
+// primitive chain open a frame: a tagged stack entry; the frame's rewrite of the hit is applied
+// when the frame closes if the closest hit was found inside it. `stk` is this lane's LDS stack
+// (stride RT_BLOCK).
+template <unsigned F, class R>
+__device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wray, double t_min, double t_max,
+                                         Hit& best, R& g, int* stk) {
+  Ray ray = wray;
+  int level = 0;
+  unsigned hitmask = 0;
+  bool found = false;
+  double closest = t_max;
+  int sp = 0;
+  int node = root;
+  for (;;) {
+    const rt_node* n = &S.nodes[node];
+    const int tf = n->type;
+    const int type = tf & RT_TYPE_MASK;
+    bool got = false, descend = false;
+    Hit h;
+    if (type == RT_NODE_BVH) {
+      if (box_hit(n->f, ray, t_min, closest)) {
+        stk[(sp++) * RT_BLOCK] = n->b;
+        node = n->a;
+        descend = true;
+      }
+    } else if ((F & F_INST) && (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE)) {
+      if (tf & RT_CHAIN_PRIM) {
+        got = chain_hit<F>(S, node, ray, t_min, closest, h);
+      } else {
+        stk[(sp++) * RT_BLOCK] = RT_FRAME | node;
+        ray = enter_instance(n, ray);
+        ++level;
+        node = n->a;
+        descend = true;
+      }
+    } else if ((F & F_MEDIA) && type == RT_NODE_CONSTANT_MEDIUM) {
+      got = medium_hit<F>(S, n, ray, t_min, closest, g, h);
+    } else {
+      got = prim_hit<F>(S, node, ray, t_min, closest, h);
+    }
+    if (got) {
+      best = h;
+      closest = h.t;
+      found = true;
+      hitmask = (1u << level) - 1u;
+    }
+    if (descend) continue;
+    // pop
+    for (;;) {
+      if (sp == 0) return found;
+      const int e = stk[(--sp) * RT_BLOCK];
+      if (!(F & F_INST) || !(e & RT_FRAME)) {
+        node = e;
+        break;
+      }
+      const rt_node* fn = &S.nodes[e & ~RT_FRAME];
+      if ((hitmask >> (level - 1)) & 1u) {
+        exit_instance(fn, ray, best);
+        hitmask &= ~(1u << (level - 1));
+      }
+      --level;
+      ray = wray;  // rebuild the parent's ray from the world ray through the still-open frames
+      for (int k = 0; k < sp; ++k) {
+        const int f = stk[k * RT_BLOCK];
+        if (f & RT_FRAME) ray = enter_instance(&S.nodes[f & ~RT_FRAME], ray);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ lights (Lib.hs:662-724)
+// htblPdfValue (Lib.hs:673-705). For a BVHNode the reference gates on hit(node) and then sums
+// the children's pdfs, each re-hit on its own. With no media in the lights tree (validated) a
+// child that is not hit contributes exactly +0, so gating on the node's box test alone gives
+// the same value: pdf(BVH) = box ? wl*(pdf(l)+0) + wr*(pdf(r)+0) : 0. Depth <= RT_LIGHT_DEPTH.
+template <unsigned F, int D>
+__device__ __forceinline__ double htbl_pdf_value(const Scene& S, int id, V3 origin, V3 v) {
+  const rt_node* n = &S.nodes[id];
+  const int type = n->type & RT_TYPE_MASK;
+  const Ray r{origin, v, 0.0};
+  Hit hh;
+  if (type == RT_NODE_RECT_XZ) {
+    if (!rect_hit(1, n->f[0], n->f[1], n->f[2], n->f[3], n->f[4], n->a, r, kEps, INFINITY, hh)) return 0.0;
+    const double area = (n->f[1] - n->f[0]) * (n->f[3] - n->f[2]);
+    const double distance_squared = hh.t * hh.t * sqlen(v);
+    const double cosine = fabs(dot(v, hh.n) / vlen(v));
+    return distance_squared / (cosine * area);
+  }
+  if (type == RT_NODE_SPHERE) {
+    if (!sphere_hit<0>(S, vload(n->f), n->f[3], n->a, r, kEps, INFINITY, hh)) return 0.0;
+    const double radius = n->f[3];
+    const double cos_theta_max = sqrt(1 - radius * radius / sqlen(vload(n->f) - origin));
+    const double solid_angle = 2 * kPi * (1 - cos_theta_max);
+    return 1 / solid_angle;
+  }
+  if constexpr (D > 0) {
+    if (type == RT_NODE_BVH) {
+      if (!box_hit(n->f, r, kEps, INFINITY)) return 0.0;
+      const double left_pdf = htbl_pdf_value<F, D - 1>(S, n->a, origin, v) + 0;
+      const double left_w = (double)S.nodes[n->a].c / (double)n->c;
+      const double right_pdf = htbl_pdf_value<F, D - 1>(S, n->b, origin, v) + 0;
+      const double right_w = (double)S.nodes[n->b].c / (double)n->c;
+      return left_w * left_pdf + right_w * right_pdf;
+    }
+  }
+  return 0.0;
+}
+
+// htblRandom (Lib.hs:707-724)
+template <class R>
+__device__ inline V3 htbl_random(const Scene& S, int id, V3 o, R& g) {
+  while (id >= 0 && (S.nodes[id].type & RT_TYPE_MASK) == RT_NODE_BVH) {
+    const rt_node* n = &S.nodes[id];
+    const double rd = g.draw();
+    id = rd < (double)S.nodes[n->a].c / (double)n->c ? n->a : n->b;
+  }
+  if (id < 0) return v3(1, 0, 0);
+  const rt_node* n = &S.nodes[id];
+  const int type = n->type & RT_TYPE_MASK;
+  if (type == RT_NODE_RECT_XZ) {
+    const double rx = draw_r(g, n->f[0], n->f[1]);
+    const double rz = draw_r(g, n->f[2], n->f[3]);
+    return v3(rx, n->f[4], rz) - o;
+  }
+  if (type == RT_NODE_SPHERE) {
+    const V3 dir = vload(n->f) - o;
+    const double dist_squared = sqlen(dir);
+    const ONB uvw = onb_from_w(dir);
+    const V3 rts = random_to_sphere(g, n->f[3], dist_squared);
+    return onb_local(uvw, rts);
+  }
+  return v3(1, 0, 0);
+}
+
+// ------------------------------------------------------------------ materials (Lib.hs:822-903)
+__device__ __forceinline__ V3 reflect(V3 v, V3 n) { return v - scale(2.0 * dot(v, n), n); }
+__device__ __forceinline__ V3 refract(V3 v, V3 n, double eta) {
+  const V3 uv = unit(v);
+  const double cos_theta = dot(vneg(uv), n);
+  const V3 par = scale(eta, uv + scale(cos_theta, n));
+  const V3 perp = scale(-sqrt(1.0 - sqlen(par)), n);
+  return par + perp;
+}
+__device__ __forceinline__ double schlick(double cosine, double ref_idx) {
+  const double r0 = (1.0 - ref_idx) / (1.0 + ref_idx);
+  const double r1 = r0 * r0;
+  return r1 + (1.0 - r1) * pow(1 - cosine, 5.0);
+}
+
+struct Scatter {
+  Ray ray;
+  V3 att;
+  double pdf;
+  int specular;
+};
+
+// scatter for every material except DiffuseLight (which the caller turns into `emitted`).
+template <unsigned F, class R>
+__device__ __forceinline__ void scatter(const Scene& S, const DMat& m, const Ray& r, const Hit& h, R& g, Scatter& s) {
+  s.ray.o = h.p;
+  s.ray.tm = r.tm;
+  if (m.type == RT_MAT_LAMBERTIAN) {  // Lib.hs:823-836, mixture of light and cosine pdfs
+    s.att = texture_value<F>(S, m.tex, h.u, h.v, h.p);
+    const ONB uvw = onb_from_w(h.n);
+    const double rd = g.draw();
+    V3 pdf_d;
+    if (rd < 0.5) pdf_d = (F & F_LIGHTS) ? htbl_random(S, S.lights, h.p, g) : v3(1, 0, 0);
+    else pdf_d = onb_local(uvw, random_cosine_direction(g));
+    const V3 dir = unit(pdf_d);
+    s.ray.d = dir;
+    double v1 = 0.0;
+    if constexpr ((F & F_LIGHTS) != 0) v1 = S.lights >= 0 ? htbl_pdf_value<F, RT_LIGHT_DEPTH>(S, S.lights, h.p, dir) : 0.0;
+    const double cosine = dot(unit(dir), uvw.w);
+    const double v2 = cosine <= 0 ? 0 : cosine / kPi;
+    s.pdf = 0.5 * (v1 + v2);
+    s.specular = 0;
+  } else if (m.type == RT_MAT_METAL) {  // Lib.hs:837-841
+    const V3 r_unit = random_unit_vector(g);
+    const V3 reflected = reflect(unit(r.d), h.n);
+    s.ray.d = reflected + scale(m.param, r_unit);
+    s.att = texture_value<F>(S, m.tex, h.u, h.v, h.p);
+    s.pdf = 0.0;
+    s.specular = 1;
+  } else if (m.type == RT_MAT_DIELECTRIC) {  // Lib.hs:842-859
+    const double eta = h.ff ? 1.0 / m.param : m.param;
+    const V3 ud = unit(r.d);
+    const double cos_theta = gmin(dot(vneg(ud), h.n), 1.0);
+    const double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
+    const double rd = g.draw();
+    if ((eta * sin_theta > 1.0) || rd < schlick(cos_theta, eta)) s.ray.d = reflect(ud, h.n);
+    else s.ray.d = refract(ud, h.n, eta);
+    s.att = v3(1.0, 1.0, 1.0);
+    s.pdf = 1.0;
+    s.specular = 1;
+  } else {  // RT_MAT_ISOTROPIC, Lib.hs:861-865
+    s.ray.d = random_in_unit_sphere(g);
+    s.att = texture_value<F>(S, m.tex, h.u, h.v, h.p);
+    s.pdf = 1.0;
+    s.specular = 0;
+  }
+}
+
+}  // namespace rtd
