@@ -260,7 +260,7 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
   g.init(seed, (uint32_t)i, 0);
   Hit h;
   double* o = out + 12 * (long long)i;
-  if (traverse<F_ALL>(S, S.world, r, tmin, tmax, h, g, stk)) {
+  if (traverse<F_ALL | F_UV>(S, S.world, r, tmin, tmax, h, g, stk)) {
     o[0] = 1; o[1] = h.t;
     o[2] = h.p.x; o[3] = h.p.y; o[4] = h.p.z;
     o[5] = h.n.x; o[6] = h.n.y; o[7] = h.n.z;

@@ -12,7 +12,8 @@ enum : unsigned {
   F_MEDIA = 8u,   // ConstantMedium (+ Isotropic)
   F_LIGHTS = 16u, // a lights tree (Lambertian light sampling / pdf)
   F_TEX = 32u,    // Checker / Perlin / Image textures (and sphere u, v)
-  F_ALL = 63u
+  F_ALL = 63u,
+  F_UV = 64u      // always compute sphere (u, v) (debug queries)
 };
 
 // ------------------------------------------------------------------ textures (Lib.hs:441-513)
@@ -136,7 +137,7 @@ __device__ __forceinline__ bool sphere_hit(const Scene& S, V3 sc, double sr, int
   const V3 outward = divide(h.p - sc, sr);
   face_normal(r, outward, h.ff, h.n);
   h.mat = sm;
-  if ((F & F_TEX) && S.mats[sm].needs_uv) {  // u, v only feed image textures; skip atan2/asin otherwise
+  if ((F & F_UV) || ((F & F_TEX) && S.mats[sm].needs_uv)) {  // u, v only feed image textures; skip atan2/asin otherwise
     const double phi = ghc_atan2(outward.z, outward.x);
     const double theta = asin(outward.y);
     h.u = 1.0 - ((phi + kPi) / (2 * kPi));

@@ -489,3 +489,36 @@ def write_ppm(rgb: np.ndarray) -> bytes:
     buf = C.create_string_buffer(n.value)
     _check(lib().rt_write_ppm(rgb.ctypes.data_as(P(C.c_uint8)), W, H, buf, n.value, C.byref(n)), "rt_write_ppm")
     return buf.raw[: n.value]
+
+
+# ----------------------------------------------------------------------------- tiling (host mirror)
+def shard_pixel_map(params: rt_render_params) -> np.ndarray:
+    """Slab work index -> image pixel index (row * W + x) or -1 for padding, for one shard.
+    Host restatement of the kernel's work_pixel() mapping (tile-major, 8x8 blocks per tile)."""
+    tt, per_shard, slab = shard_geometry(params)
+    tile = params.tile or 16
+    shards = max(1, params.shard_count)
+    tiles_x = (params.width + tile - 1) // tile
+    w = np.arange(slab, dtype=np.int64)
+    tp = tile * tile
+    lt, within = w // tp, w % tp
+    gt = params.shard_rank + lt * shards
+    blk, lane = within >> 6, within & 63
+    bpr = tile >> 3
+    px = (gt % tiles_x) * tile + (blk % bpr) * 8 + (lane & 7)
+    row = (gt // tiles_x) * tile + (blk // bpr) * 8 + (lane >> 3)
+    ok = (gt < tt) & (px < params.width) & (row < params.height)
+    return np.where(ok, row * params.width + px, -1)
+
+
+def assemble_host(slabs: np.ndarray, params: rt_render_params) -> np.ndarray:
+    """Host restatement of the assemble kernel: (shards, slab, 3) -> (H, W, 3)."""
+    W, H = params.width, params.height
+    img = np.zeros((H * W, 3), dtype=slabs.dtype)
+    for r in range(slabs.shape[0]):
+        p = make_params(W, H, params.spp, params.max_depth, params.rng_mode, params.seed, params.flags,
+                        params.tile, r, slabs.shape[0])
+        m = shard_pixel_map(p)
+        ok = m >= 0
+        img[m[ok]] = slabs[r][ok]
+    return img.reshape(H, W, 3)

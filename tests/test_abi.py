@@ -1,0 +1,78 @@
+"""C-ABI checks without a GPU: the library loads, exports exactly what include/rt.h declares,
+validates arguments, and writes the reference's P3 format."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+import rtamd
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "rt.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_every_declared_symbol_is_exported():
+    L = rtamd.lib()
+    declared = _declared()
+    assert len(declared) >= 40
+    missing = [s for s in declared if not hasattr(L, s)]
+    assert not missing, missing
+    assert sorted(rtamd.EXPORTED) == declared
+
+
+def test_abi_version():
+    assert rtamd.lib().rt_abi_version() == 1
+
+
+def test_struct_sizes_match_header():
+    assert C.sizeof(rtamd.rt_node) == 64
+    assert C.sizeof(rtamd.rt_scene_desc) == 112
+    assert C.sizeof(rtamd.rt_render_params) == 48
+
+
+def test_param_validation_without_gpu():
+    with pytest.raises(rtamd.RTError):
+        rtamd.shard_geometry(rtamd.make_params(0, 10, 1, 1))
+    with pytest.raises(rtamd.RTError):
+        rtamd.shard_geometry(rtamd.make_params(10, 10, 1, 1, tile=12))
+    with pytest.raises(rtamd.RTError):
+        rtamd.shard_geometry(rtamd.make_params(10, 10, 1, 1, shard_rank=2, shard_count=2))
+    tt, per, slab = rtamd.shard_geometry(rtamd.make_params(1200, 800, 1, 1, tile=16, shard_count=8))
+    assert tt == 75 * 50 and per == (3750 + 7) // 8 and slab == per * 256
+
+
+def test_ppm_matches_printrow():
+    """P3 / "W H" / 255, then one line per row of space-separated components (src/Lib.hs:299-305)."""
+    rgb = np.random.default_rng(0).integers(0, 256, (3, 4, 3), dtype=np.uint8)
+    txt = rtamd.write_ppm(rgb).decode()
+    lines = txt.split("\n")
+    assert lines[0] == "P3" and lines[1] == "4 3" and lines[2] == "255"
+    for r in range(3):
+        assert lines[3 + r] == " ".join(str(int(v)) for v in rgb[r].reshape(-1))
+    assert txt.endswith("\n") and len(lines) == 3 + 3 + 1
+
+
+def test_tile_map_is_a_partition():
+    """Across shards, every pixel is owned exactly once (the gather is a permutation)."""
+    for W, H, tile, n in [(1200, 800, 16, 8), (97, 61, 16, 3), (200, 100, 8, 2), (33, 17, 32, 5)]:
+        seen = np.zeros(W * H, dtype=np.int64)
+        for r in range(n):
+            m = rtamd.shard_pixel_map(rtamd.make_params(W, H, 1, 1, tile=tile, shard_rank=r, shard_count=n))
+            np.add.at(seen, m[m >= 0], 1)
+        assert (seen == 1).all()
+
+
+def test_render_without_device_fails_loudly():
+    """No CPU fallback: creating a device context on a box with no GPU raises."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(rtamd.RTError):
+        rtamd.Context(0)
