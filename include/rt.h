@@ -177,6 +177,9 @@ typedef struct rt_camera {
 #define RT_FLAG_NAN_CULL 1u /* tier B only: stop tracing a pixel once its sum is NaN
                                (its output byte is then fixed at 0, src/Lib.hs:287-288).
                                Output-identical; off by default. */
+#define RT_FLAG_REFERENCE_CULL 2u /* cull BVH boxes with the reference's per-axis test only
+                               (src/Lib.hs:798-814). Default: that test AND the joint slab test,
+                               which only prunes boxes that cannot hold a hit. */
 
 typedef struct rt_render_params {
     int32_t width;
@@ -327,7 +330,14 @@ int rt_last_kernel_ms(rt_ctx* ctx, double* out_ms);
  * material. Media draws use tier-B stream (seed, pixel_id = ray index, sample 0).
  */
 int rt_debug_closest_hits(rt_ctx* ctx, const double* rays, int n, double tmin, double tmax,
-                          uint64_t seed, double* out);
+                          uint64_t seed, uint32_t flags, double* out);
+
+/*
+ * Debug / numerics probe: out[i] = op(x[i], y[i]) evaluated on the device.
+ * ops: 0 x/y (IEEE), 1 div_exact(x, y) (reciprocal + Markstein), 2 sqrt x, 3 sin x, 4 cos x,
+ * 5 atan x, 6 asin x, 7 log x, 8 pow(x, y), 9 GHC atan2(x, y), 10 tan x.
+ */
+int rt_debug_math(rt_ctx* ctx, int op, const double* x, const double* y, int n, double* out);
 
 #ifdef __cplusplus
 }

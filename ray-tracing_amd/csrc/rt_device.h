@@ -53,6 +53,53 @@ struct Ray {
   V3 o, d;
   double tm;
 };
+
+// Correctly rounded a / b from y = RN(1/b): two Markstein residual corrections (each residual
+// a - b*q is exact under FMA), then a range guard that falls back to the IEEE division whenever
+// the quotient is zero, tiny, huge or not finite. Bit-identical to `a / b` (tests/test_gpu_math).
+__device__ __forceinline__ double div_exact(double a, double b, double y) {
+  double q = a * y;
+  double r = fma(-q, b, a);
+  q = fma(r, y, q);
+  r = fma(-q, b, a);
+  q = fma(r, y, q);
+  const double aq = fabs(q);
+  if (!(aq >= 0x1p-900 && aq <= 0x1p900)) q = a / b;
+  return q;
+}
+
+// A ray plus the per-ray reciprocals the exact divisions use. `safe` = every divisor in
+// [2^-500, 2^500] (else all divisions take the IEEE path).
+struct RayX {
+  V3 o, d;
+  double tm;
+  V3 inv;      // RN(1 / d)
+  double a;    // dot d d (the sphere quadratic's `a`, Lib.hs:1092)
+  double inva; // RN(1 / a)
+  bool safe;
+};
+__device__ __forceinline__ bool div_ok(double b) {
+  const double ab = fabs(b);
+  return ab >= 0x1p-500 && ab <= 0x1p500;
+}
+__device__ __forceinline__ RayX prep(const Ray& r) {
+  RayX x;
+  x.o = r.o;
+  x.d = r.d;
+  x.tm = r.tm;
+  x.inv = V3{1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z};
+  x.a = r.d.x * r.d.x + r.d.y * r.d.y + r.d.z * r.d.z;
+  x.inva = 1.0 / x.a;
+  x.safe = div_ok(r.d.x) && div_ok(r.d.y) && div_ok(r.d.z) && div_ok(x.a);
+  return x;
+}
+__device__ __forceinline__ Ray plain(const RayX& x) { return Ray{x.o, x.d, x.tm}; }
+// q = a / d_axis, exactly
+__device__ __forceinline__ double divd(const RayX& r, double a, int axis) {
+  const double d = axis == 0 ? r.d.x : (axis == 1 ? r.d.y : r.d.z);
+  const double y = axis == 0 ? r.inv.x : (axis == 1 ? r.inv.y : r.inv.z);
+  return r.safe ? div_exact(a, d, y) : a / d;
+}
 struct Hit {
   double t;
   V3 p, n;

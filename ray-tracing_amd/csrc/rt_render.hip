@@ -103,7 +103,7 @@ __device__ __forceinline__ bool segment(const RenderArgs& A, Ray& ray, V3& thr, 
     return true;
   }
   Hit h;
-  if (!traverse<F>(S, S.world, ray, kEps, INFINITY, h, g, stk)) {
+  if (!traverse<F>(S, S.world, ray, kEps, INFINITY, h, g, stk, !(A.flags & RT_FLAG_REFERENCE_CULL))) {
     contrib = vmul(thr, v3(S.bg[0], S.bg[1], S.bg[2]));
     return true;
   }
@@ -249,7 +249,7 @@ __global__ void assemble(const T* slabs, T* image, int W, int H, int tile, int t
 
 // ---------------------------------------------------------------- debug: closest hits
 __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* rays, int n, double tmin,
-                                                         double tmax, uint64_t seed, double* out) {
+                                                         double tmax, uint64_t seed, int joint, double* out) {
   __shared__ int stk_mem[RT_STACK * RT_BLOCK];
   int* stk = &stk_mem[threadIdx.x];
   const int i = blockIdx.x * RT_BLOCK + threadIdx.x;
@@ -260,7 +260,7 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
   g.init(seed, (uint32_t)i, 0);
   Hit h;
   double* o = out + 12 * (long long)i;
-  if (traverse<F_ALL | F_UV>(S, S.world, r, tmin, tmax, h, g, stk)) {
+  if (traverse<F_ALL | F_UV>(S, S.world, r, tmin, tmax, h, g, stk, joint != 0)) {
     o[0] = 1; o[1] = h.t;
     o[2] = h.p.x; o[3] = h.p.y; o[4] = h.p.z;
     o[5] = h.n.x; o[6] = h.n.y; o[7] = h.n.z;
@@ -268,6 +268,28 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
   } else {
     for (int k = 0; k < 12; ++k) o[k] = 0;
   }
+}
+
+// ---------------------------------------------------------------- debug: numerics probe
+__global__ void math_probe(int op, const double* x, const double* y, int n, double* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double a = x[i], b = y[i];
+  double r;
+  switch (op) {
+    case 0: r = a / b; break;
+    case 1: r = div_exact(a, b, 1.0 / b); break;
+    case 2: r = sqrt(a); break;
+    case 3: r = sin(a); break;
+    case 4: r = cos(a); break;
+    case 5: r = atan(a); break;
+    case 6: r = asin(a); break;
+    case 7: r = log(a); break;
+    case 8: r = pow(a, b); break;
+    case 9: r = ghc_atan2(a, b); break;
+    default: r = tan(a); break;
+  }
+  out[i] = r;
 }
 
 }  // namespace
@@ -785,7 +807,8 @@ int rt_last_kernel_ms(rt_ctx* c, double* out_ms) {
   return RT_OK;
 }
 
-int rt_debug_closest_hits(rt_ctx* c, const double* rays, int n, double tmin, double tmax, uint64_t seed, double* out) {
+int rt_debug_closest_hits(rt_ctx* c, const double* rays, int n, double tmin, double tmax, uint64_t seed,
+                          uint32_t flags, double* out) {
   if (!c || !rays || !out || n < 0) return invalid("null argument");
   if (!c->has_scene) {
     rt::set_error("rt_debug_closest_hits: no scene uploaded");
@@ -798,12 +821,33 @@ int rt_debug_closest_hits(rt_ctx* c, const double* rays, int n, double tmin, dou
   HIPCHK(hipMalloc((void**)&d_out, sizeof(double) * 12 * (size_t)n));
   HIPCHK(hipMemcpy(d_rays, rays, sizeof(double) * 7 * (size_t)n, hipMemcpyHostToDevice));
   hipLaunchKernelGGL(closest_hits, dim3((n + RT_BLOCK - 1) / RT_BLOCK), dim3(RT_BLOCK), 0, c->stream, c->scene,
-                     d_rays, n, tmin, tmax, seed, d_out);
+                     d_rays, n, tmin, tmax, seed, (int)!(flags & RT_FLAG_REFERENCE_CULL), d_out);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipMemcpy(out, d_out, sizeof(double) * 12 * (size_t)n, hipMemcpyDeviceToHost));
   (void)hipFree(d_rays);
   (void)hipFree(d_out);
+  return RT_OK;
+}
+
+int rt_debug_math(rt_ctx* c, int op, const double* x, const double* y, int n, double* out) {
+  if (!c || !x || !y || !out || n < 0 || op < 0 || op > 10) return invalid("rt_debug_math: bad argument");
+  if (n == 0) return RT_OK;
+  HIPCHK(hipSetDevice(c->device));
+  double *dx = nullptr, *dy = nullptr, *dout = nullptr;
+  const size_t bytes = sizeof(double) * (size_t)n;
+  HIPCHK(hipMalloc((void**)&dx, bytes));
+  HIPCHK(hipMalloc((void**)&dy, bytes));
+  HIPCHK(hipMalloc((void**)&dout, bytes));
+  HIPCHK(hipMemcpy(dx, x, bytes, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dy, y, bytes, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(math_probe, dim3((n + 255) / 256), dim3(256), 0, c->stream, op, dx, dy, n, dout);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost));
+  (void)hipFree(dx);
+  (void)hipFree(dy);
+  (void)hipFree(dout);
   return RT_OK;
 }
 

@@ -79,32 +79,79 @@ __device__ inline V3 texture_value(const Scene& S, int tid, double u, double v, 
 }
 
 // ------------------------------------------------------------------ primitives
-// boxRayIntersect (Lib.hs:798-814): per-axis slab with true division, GHC max/min.
-__device__ __forceinline__ bool box_hit(const double* f, const Ray& r, double t_min, double t_max) {
-  bool ok = true;
+// Unguarded Markstein quotient and the range it is trusted in (see div_exact in rt_device.h).
+__device__ __forceinline__ double div_mk(double a, double b, double y) {
+  double q = a * y;
+  double r = fma(-q, b, a);
+  q = fma(r, y, q);
+  r = fma(-q, b, a);
+  return fma(r, y, q);
+}
+__device__ __forceinline__ bool q_ok(double q) {
+  const double aq = fabs(q);
+  return aq >= 0x1p-900 && aq <= 0x1p900;
+}
+
+// boxRayIntersect (Lib.hs:798-814): per axis, [max t0 t_min, min t1 t_max] must be non-empty,
+// with the reference's quotients (bit-exact) and GHC max/min. The reference never intersects the
+// three axis intervals; with `joint` the box must ALSO pass the joint slab test (max of the axis
+// lower bounds < min of the upper bounds). That accepts a subset of the reference's boxes, so it
+// only prunes subtrees; what it prunes cannot hold a hit in [t_min, t_max] except exactly on a box
+// face (measure zero; tests/test_gpu_parity.py checks closest hits bit for bit).
+__device__ __forceinline__ bool box_hit(const double* f, const RayX& r, double t_min, double t_max, bool joint) {
+  double q[6];
+  bool good = r.safe;
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
-    const double o = comp(r.o, a), d = comp(r.d, a);
-    const double ta = (f[a] - o) / d;
-    const double tb = (f[a + 3] - o) / d;
+    const double o = comp(r.o, a), d = comp(r.d, a), y = comp(r.inv, a);
+    q[2 * a] = div_mk(f[a] - o, d, y);
+    q[2 * a + 1] = div_mk(f[a + 3] - o, d, y);
+    good = good && q_ok(q[2 * a]) && q_ok(q[2 * a + 1]);
+  }
+  if (!good) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const double o = comp(r.o, a), d = comp(r.d, a);
+      q[2 * a] = (f[a] - o) / d;
+      q[2 * a + 1] = (f[a + 3] - o) / d;
+    }
+  }
+  bool ok = true;
+  double lmax = t_min, hmin = t_max;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const double ta = q[2 * a], tb = q[2 * a + 1];
     const bool lt = ta < tb;
     const double t0 = lt ? ta : tb, t1 = lt ? tb : ta;
     const double lo = gmax(t0, t_min);
     const double hi = gmin(t1, t_max);
     ok = ok && (hi > lo);
+    lmax = lo > lmax ? lo : lmax;
+    hmin = hi < hmin ? hi : hmin;
   }
-  return ok;
+  return ok && (!joint || hmin > lmax);
 }
 
-// rectHit (Lib.hs:1005-1028); plane 0 XY, 1 XZ, 2 YZ. Rejects only t < tmin or t > tmax.
-__device__ __forceinline__ bool rect_hit(int plane, double i0, double i1, double j0, double j1, double k, int mat,
-                                         const Ray& r, double t_min, double t_max, Hit& h) {
+// rectHit's t (Lib.hs:1014-1028); plane 0 XY, 1 XZ, 2 YZ. Rejects only t < tmin or t > tmax
+// (t == tmax is a hit; a NaN t passes). Returns the t of a hit.
+__device__ __forceinline__ bool rect_t(int plane, double i0, double i1, double j0, double j1, double k,
+                                       const RayX& r, double t_min, double t_max, double& tout) {
   const int ii = plane == 2 ? 1 : 0, jj = plane == 0 ? 1 : 2, kk = plane == 0 ? 2 : (plane == 1 ? 1 : 0);
-  const double t = (k - comp(r.o, kk)) / comp(r.d, kk);
+  const double num = k - comp(r.o, kk);
+  double t = r.safe ? div_mk(num, comp(r.d, kk), comp(r.inv, kk)) : 0.0;
+  if (!r.safe || !q_ok(t)) t = num / comp(r.d, kk);
   if ((t < t_min) || (t > t_max)) return false;
   const double i = comp(r.o, ii) + t * comp(r.d, ii);
   const double j = comp(r.o, jj) + t * comp(r.d, jj);
   if ((i < i0) || (i > i1) || (j < j0) || (j > j1)) return false;
+  tout = t;
+  return true;
+}
+__device__ __forceinline__ void rect_record(int plane, double i0, double i1, double j0, double j1, int mat,
+                                            const Ray& r, double t, Hit& h) {
+  const int ii = plane == 2 ? 1 : 0, jj = plane == 0 ? 1 : 2;
+  const double i = comp(r.o, ii) + t * comp(r.d, ii);
+  const double j = comp(r.o, jj) + t * comp(r.d, jj);
   h.t = t;
   h.u = (i - i0) / (i1 - i0);
   h.v = (j - j0) / (j1 - j0);
@@ -112,32 +159,46 @@ __device__ __forceinline__ bool rect_hit(int plane, double i0, double i1, double
   const V3 outward = plane == 0 ? v3(0, 0, 1) : (plane == 1 ? v3(0, 1, 0) : v3(1, 0, 0));
   face_normal(r, outward, h.ff, h.n);
   h.mat = mat;
+}
+// full rectHit (record included), for the light pdf and cuboid faces
+__device__ __forceinline__ bool rect_hit(int plane, double i0, double i1, double j0, double j1, double k, int mat,
+                                         const RayX& r, double t_min, double t_max, Hit& h) {
+  double t;
+  if (!rect_t(plane, i0, i1, j0, j1, k, r, t_min, t_max, t)) return false;
+  rect_record(plane, i0, i1, j0, j1, mat, plain(r), t, h);
   return true;
 }
 
-// hit Sphere (Lib.hs:1081-1105): strict tmin < t < tmax.
-template <unsigned F>
-__device__ __forceinline__ bool sphere_hit(const Scene& S, V3 sc, double sr, int sm, const Ray& r, double t_min,
-                                           double t_max, Hit& h) {
+// hit Sphere's t (Lib.hs:1081-1095): strict tmin < t < tmax, quotients exact.
+__device__ __forceinline__ bool sphere_t(V3 sc, double sr, const RayX& r, double t_min, double t_max, double& tout) {
   const V3 oc = r.o - sc;
-  const double a = dot(r.d, r.d);
+  const double a = r.a;
   const double b = dot(oc, r.d);
   const double c = dot(oc, oc) - (sr * sr);
   const double disc = b * b - a * c;
   if (!(disc > 0)) return false;
   const double sd = sqrt(disc);
-  const double temp1 = ((-b) - sd) / a;
-  const double temp2 = ((-b) + sd) / a;
-  double temp;
-  if (t_min < temp1 && temp1 < t_max) temp = temp1;
-  else if (t_min < temp2 && temp2 < t_max) temp = temp2;
+  const double n1 = (-b) - sd, n2 = (-b) + sd;
+  double temp1 = div_mk(n1, a, r.inva), temp2 = div_mk(n2, a, r.inva);
+  if (!(r.safe && q_ok(temp1) && q_ok(temp2))) {
+    temp1 = n1 / a;
+    temp2 = n2 / a;
+  }
+  if (t_min < temp1 && temp1 < t_max) tout = temp1;
+  else if (t_min < temp2 && temp2 < t_max) tout = temp2;
   else return false;
-  h.t = temp;
-  h.p = at(r, temp);
+  return true;
+}
+// the rest of hit Sphere (Lib.hs:1096-1105)
+template <unsigned F>
+__device__ __forceinline__ void sphere_record(const Scene& S, V3 sc, double sr, int sm, const Ray& r, double t,
+                                              Hit& h) {
+  h.t = t;
+  h.p = at(r, t);
   const V3 outward = divide(h.p - sc, sr);
   face_normal(r, outward, h.ff, h.n);
   h.mat = sm;
-  if ((F & F_UV) || ((F & F_TEX) && S.mats[sm].needs_uv)) {  // u, v only feed image textures; skip atan2/asin otherwise
+  if ((F & F_UV) || ((F & F_TEX) && S.mats[sm].needs_uv)) {  // u, v only feed image textures
     const double phi = ghc_atan2(outward.z, outward.x);
     const double theta = asin(outward.y);
     h.u = 1.0 - ((phi + kPi) / (2 * kPi));
@@ -146,44 +207,80 @@ __device__ __forceinline__ bool sphere_hit(const Scene& S, V3 sc, double sr, int
     h.u = 0.0;
     h.v = 0.0;
   }
+}
+template <unsigned F>
+__device__ __forceinline__ bool sphere_hit(const Scene& S, V3 sc, double sr, int sm, const RayX& r, double t_min,
+                                           double t_max, Hit& h) {
+  double t;
+  if (!sphere_t(sc, sr, r, t_min, t_max, t)) return false;
+  sphere_record<F>(S, sc, sr, sm, plain(r), t, h);
   return true;
 }
 
-// Leaf primitives: Sphere, MovingSphere, Rect{XY,XZ,YZ}, Cuboid.
+// One face of a cuboid (Lib.hs:599-604): face i -> plane and bounds.
+__device__ __forceinline__ void cuboid_face(const rt_node* n, int i, int& plane, double& a0, double& a1, double& b0,
+                                            double& b1, double& k) {
+  const double x0 = n->f[0], y0 = n->f[1], z0 = n->f[2], x1 = n->f[3], y1 = n->f[4], z1 = n->f[5];
+  plane = i >> 1;
+  a0 = plane == 2 ? y0 : x0;
+  a1 = plane == 2 ? y1 : x1;
+  b0 = plane == 0 ? y0 : z0;
+  b1 = plane == 0 ? y1 : z1;
+  k = (i & 1) ? (plane == 0 ? z0 : (plane == 1 ? y0 : x0)) : (plane == 0 ? z1 : (plane == 1 ? y1 : x1));
+}
+
+// Leaf primitives (Sphere, MovingSphere, Rect{XY,XZ,YZ}, Cuboid): the t of a hit and, for a
+// cuboid, which face (`sub`) won. hit Cuboid (Lib.hs:989-1004) is foldr closerHit over the six
+// faces, each with the full [tmin, tmax]: the later face keeps a tie.
 template <unsigned F>
-__device__ inline bool prim_hit(const Scene& S, int id, const Ray& r, double t_min, double t_max, Hit& h) {
-  const rt_node* n = &S.nodes[id];
+__device__ __forceinline__ bool prim_t(const Scene& S, const rt_node* n, const RayX& r, double t_min, double t_max,
+                                       double& t, int& sub) {
   const int type = n->type & RT_TYPE_MASK;
-  if (!(F & (F_RECT | F_MOVING)) || type == RT_NODE_SPHERE)
-    return sphere_hit<F>(S, vload(n->f), n->f[3], n->a, r, t_min, t_max, h);
+  sub = 0;
+  if (!(F & (F_RECT | F_MOVING)) || type == RT_NODE_SPHERE) return sphere_t(vload(n->f), n->f[3], r, t_min, t_max, t);
   if ((F & F_MOVING) && type == RT_NODE_MOVING_SPHERE) {  // Lib.hs:1106-1108
     const rt_node* e = n + 1;
     const V3 c0 = vload(n->f), c1 = vload(n->f + 3);
     const V3 sc = c0 + scale((r.tm - e->f[0]) / e->f[2], c1 - c0);
-    return sphere_hit<F>(S, sc, e->f[3], n->a, r, t_min, t_max, h);
+    return sphere_t(sc, e->f[3], r, t_min, t_max, t);
   }
   if constexpr (!(F & F_RECT)) return false;
-  if (type == RT_NODE_CUBOID) {  // Lib.hs:989-1004: foldr closerHit; ties go to the later face
-    const double x0 = n->f[0], y0 = n->f[1], z0 = n->f[2], x1 = n->f[3], y1 = n->f[4], z1 = n->f[5];
+  if (type == RT_NODE_CUBOID) {
     bool have = false;
     for (int i = 5; i >= 0; --i) {
-      const int plane = i >> 1;
-      const double a0 = plane == 2 ? y0 : x0, a1 = plane == 2 ? y1 : x1;
-      const double b0 = plane == 0 ? y0 : z0, b1 = plane == 0 ? y1 : z1;
-      const double k = (i & 1) ? (plane == 0 ? z0 : (plane == 1 ? y0 : x0)) : (plane == 0 ? z1 : (plane == 1 ? y1 : x1));
-      Hit hh;
-      if (rect_hit(plane, a0, a1, b0, b1, k, n->a, r, t_min, t_max, hh)) {
-        if (!have || hh.t < h.t) {
-          h = hh;
-          have = true;
-        }
+      int plane;
+      double a0, a1, b0, b1, k, tt;
+      cuboid_face(n, i, plane, a0, a1, b0, b1, k);
+      if (rect_t(plane, a0, a1, b0, b1, k, r, t_min, t_max, tt) && (!have || tt < t)) {
+        t = tt;
+        sub = i;
+        have = true;
       }
     }
     return have;
   }
   if (type >= RT_NODE_RECT_XY && type <= RT_NODE_RECT_YZ)
-    return rect_hit(type - RT_NODE_RECT_XY, n->f[0], n->f[1], n->f[2], n->f[3], n->f[4], n->a, r, t_min, t_max, h);
+    return rect_t(type - RT_NODE_RECT_XY, n->f[0], n->f[1], n->f[2], n->f[3], n->f[4], r, t_min, t_max, t);
   return false;
+}
+template <unsigned F>
+__device__ __forceinline__ void prim_record(const Scene& S, const rt_node* n, int sub, const Ray& r, double t, Hit& h) {
+  const int type = n->type & RT_TYPE_MASK;
+  if (!(F & (F_RECT | F_MOVING)) || type == RT_NODE_SPHERE) {
+    sphere_record<F>(S, vload(n->f), n->f[3], n->a, r, t, h);
+  } else if ((F & F_MOVING) && type == RT_NODE_MOVING_SPHERE) {
+    const rt_node* e = n + 1;
+    const V3 c0 = vload(n->f), c1 = vload(n->f + 3);
+    const V3 sc = c0 + scale((r.tm - e->f[0]) / e->f[2], c1 - c0);
+    sphere_record<F>(S, sc, e->f[3], n->a, r, t, h);
+  } else if (type == RT_NODE_CUBOID) {
+    int plane;
+    double a0, a1, b0, b1, k;
+    cuboid_face(n, sub, plane, a0, a1, b0, b1, k);
+    rect_record(plane, a0, a1, b0, b1, n->a, r, t, h);
+  } else {
+    rect_record(type - RT_NODE_RECT_XY, n->f[0], n->f[1], n->f[2], n->f[3], n->a, r, t, h);
+  }
 }
 
 // One instance transform applied to the ray handed to the child (Lib.hs:1029-1031, 1038-1043).
@@ -208,17 +305,22 @@ __device__ __forceinline__ void exit_instance(const rt_node* n, const Ray& rc, H
 // A Translate/Rotate chain that ends in a leaf primitive (or the leaf itself), hit as one unit.
 template <unsigned F>
 __device__ inline bool chain_hit(const Scene& S, int id, const Ray& ray, double t_min, double t_max, Hit& h) {
-  if constexpr (!(F & F_INST)) return prim_hit<F>(S, id, ray, t_min, t_max, h);
   Ray r = ray;
   int cur = id, depth = 0;
-  while (true) {
-    const int type = S.nodes[cur].type & RT_TYPE_MASK;
-    if (type != RT_NODE_TRANSLATE && type != RT_NODE_ROTATE) break;
-    r = enter_instance(&S.nodes[cur], r);
-    cur = S.nodes[cur].a;
-    ++depth;
+  if constexpr ((F & F_INST) != 0) {
+    while (true) {
+      const int type = S.nodes[cur].type & RT_TYPE_MASK;
+      if (type != RT_NODE_TRANSLATE && type != RT_NODE_ROTATE) break;
+      r = enter_instance(&S.nodes[cur], r);
+      cur = S.nodes[cur].a;
+      ++depth;
+    }
   }
-  if (!prim_hit<F>(S, cur, r, t_min, t_max, h)) return false;
+  double t;
+  int sub;
+  const rt_node* leaf = &S.nodes[cur];
+  if (!prim_t<F>(S, leaf, prep(r), t_min, t_max, t, sub)) return false;
+  prim_record<F>(S, leaf, sub, r, t, h);
   for (int lv = depth - 1; lv >= 0; --lv) {  // rewrite from the innermost instance outwards
     Ray rl = ray;
     int nd = id;
@@ -262,57 +364,81 @@ __device__ inline bool medium_hit(const Scene& S, const rt_node* n, const Ray& r
 // ------------------------------------------------------------------ traversal
 // Closest hit over the DAG rooted at `root` in [t_min, t_max] (hit, Lib.hs:970-1109).
 // Depth-first, left child first, each visit bounded by the closest hit so far: exactly the
-// reference's recursion (including media draw order). Instances whose subtree is not a plain
-// primitive chain open a frame: a tagged stack entry; the frame's rewrite of the hit is applied
-// when the frame closes if the closest hit was found inside it. `stk` is this lane's LDS stack
-// (stride RT_BLOCK).
+// reference's recursion (including media draw order). A plain primitive hit at the top level
+// records only (t, node, face); its record is built once at the end from the same ray with the
+// same operations. Instances whose subtree is not a primitive chain open a frame (a tagged stack
+// entry); the frame's rewrite of the hit is applied when the frame closes if the closest hit was
+// found inside it. `stk` is this lane's LDS stack (stride RT_BLOCK).
 template <unsigned F, class R>
-__device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wray, double t_min, double t_max,
-                                         Hit& best, R& g, int* stk) {
-  Ray ray = wray;
+__device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr, double t_min, double t_max,
+                                         Hit& best, R& g, int* stk, bool joint) {
+  const RayX wray = prep(wr);
+  RayX ray = wray;
   int level = 0;
   unsigned hitmask = 0;
-  bool found = false;
   double closest = t_max;
+  int best_node = -1, best_sub = 0;
+  bool best_full = false;  // `best` already holds the record
   int sp = 0;
   int node = root;
   for (;;) {
     const rt_node* n = &S.nodes[node];
     const int tf = n->type;
     const int type = tf & RT_TYPE_MASK;
-    bool got = false, descend = false;
-    Hit h;
     if (type == RT_NODE_BVH) {
-      if (box_hit(n->f, ray, t_min, closest)) {
+      if (box_hit(n->f, ray, t_min, closest, joint)) {
         stk[(sp++) * RT_BLOCK] = n->b;
         node = n->a;
-        descend = true;
+        continue;
       }
     } else if ((F & F_INST) && (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE)) {
       if (tf & RT_CHAIN_PRIM) {
-        got = chain_hit<F>(S, node, ray, t_min, closest, h);
+        Hit h;
+        if (chain_hit<F>(S, node, plain(ray), t_min, closest, h)) {
+          best = h;
+          closest = h.t;
+          best_node = node;
+          best_full = true;
+          hitmask = (1u << level) - 1u;
+        }
       } else {
         stk[(sp++) * RT_BLOCK] = RT_FRAME | node;
-        ray = enter_instance(n, ray);
+        ray = prep(enter_instance(n, plain(ray)));
         ++level;
         node = n->a;
-        descend = true;
+        continue;
       }
     } else if ((F & F_MEDIA) && type == RT_NODE_CONSTANT_MEDIUM) {
-      got = medium_hit<F>(S, n, ray, t_min, closest, g, h);
+      Hit h;
+      if (medium_hit<F>(S, n, plain(ray), t_min, closest, g, h)) {
+        best = h;
+        closest = h.t;
+        best_node = node;
+        best_full = true;
+        hitmask = (1u << level) - 1u;
+      }
     } else {
-      got = prim_hit<F>(S, node, ray, t_min, closest, h);
+      double t;
+      int sub;
+      if (prim_t<F>(S, n, ray, t_min, closest, t, sub)) {
+        closest = t;
+        best_node = node;
+        best_sub = sub;
+        best_full = false;
+        if ((F & F_INST) && level > 0) {  // inside a frame: the record is needed in this frame's space
+          prim_record<F>(S, n, sub, plain(ray), t, best);
+          best_full = true;
+          hitmask = (1u << level) - 1u;
+        }
+      }
     }
-    if (got) {
-      best = h;
-      closest = h.t;
-      found = true;
-      hitmask = (1u << level) - 1u;
-    }
-    if (descend) continue;
     // pop
     for (;;) {
-      if (sp == 0) return found;
+      if (sp == 0) {
+        if (best_node < 0) return false;
+        if (!best_full) prim_record<F>(S, &S.nodes[best_node], best_sub, wr, closest, best);
+        return true;
+      }
       const int e = stk[(--sp) * RT_BLOCK];
       if (!(F & F_INST) || !(e & RT_FRAME)) {
         node = e;
@@ -320,15 +446,16 @@ __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr
       }
       const rt_node* fn = &S.nodes[e & ~RT_FRAME];
       if ((hitmask >> (level - 1)) & 1u) {
-        exit_instance(fn, ray, best);
+        exit_instance(fn, plain(ray), best);
         hitmask &= ~(1u << (level - 1));
       }
       --level;
-      ray = wray;  // rebuild the parent's ray from the world ray through the still-open frames
+      Ray pr = wr;  // rebuild the parent's ray from the world ray through the still-open frames
       for (int k = 0; k < sp; ++k) {
         const int f = stk[k * RT_BLOCK];
-        if (f & RT_FRAME) ray = enter_instance(&S.nodes[f & ~RT_FRAME], ray);
+        if (f & RT_FRAME) pr = enter_instance(&S.nodes[f & ~RT_FRAME], pr);
       }
+      ray = prep(pr);
     }
   }
 }
@@ -339,10 +466,9 @@ __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr
 // child that is not hit contributes exactly +0, so gating on the node's box test alone gives
 // the same value: pdf(BVH) = box ? wl*(pdf(l)+0) + wr*(pdf(r)+0) : 0. Depth <= RT_LIGHT_DEPTH.
 template <unsigned F, int D>
-__device__ __forceinline__ double htbl_pdf_value(const Scene& S, int id, V3 origin, V3 v) {
+__device__ __forceinline__ double htbl_pdf_value(const Scene& S, int id, V3 origin, V3 v, const RayX& r) {
   const rt_node* n = &S.nodes[id];
   const int type = n->type & RT_TYPE_MASK;
-  const Ray r{origin, v, 0.0};
   Hit hh;
   if (type == RT_NODE_RECT_XZ) {
     if (!rect_hit(1, n->f[0], n->f[1], n->f[2], n->f[3], n->f[4], n->a, r, kEps, INFINITY, hh)) return 0.0;
@@ -352,7 +478,8 @@ __device__ __forceinline__ double htbl_pdf_value(const Scene& S, int id, V3 orig
     return distance_squared / (cosine * area);
   }
   if (type == RT_NODE_SPHERE) {
-    if (!sphere_hit<0>(S, vload(n->f), n->f[3], n->a, r, kEps, INFINITY, hh)) return 0.0;
+    double t;
+    if (!sphere_t(vload(n->f), n->f[3], r, kEps, INFINITY, t)) return 0.0;
     const double radius = n->f[3];
     const double cos_theta_max = sqrt(1 - radius * radius / sqlen(vload(n->f) - origin));
     const double solid_angle = 2 * kPi * (1 - cos_theta_max);
@@ -360,10 +487,10 @@ __device__ __forceinline__ double htbl_pdf_value(const Scene& S, int id, V3 orig
   }
   if constexpr (D > 0) {
     if (type == RT_NODE_BVH) {
-      if (!box_hit(n->f, r, kEps, INFINITY)) return 0.0;
-      const double left_pdf = htbl_pdf_value<F, D - 1>(S, n->a, origin, v) + 0;
+      if (!box_hit(n->f, r, kEps, INFINITY, false)) return 0.0;
+      const double left_pdf = htbl_pdf_value<F, D - 1>(S, n->a, origin, v, r) + 0;
       const double left_w = (double)S.nodes[n->a].c / (double)n->c;
-      const double right_pdf = htbl_pdf_value<F, D - 1>(S, n->b, origin, v) + 0;
+      const double right_pdf = htbl_pdf_value<F, D - 1>(S, n->b, origin, v, r) + 0;
       const double right_w = (double)S.nodes[n->b].c / (double)n->c;
       return left_w * left_pdf + right_w * right_pdf;
     }
@@ -434,7 +561,8 @@ __device__ __forceinline__ void scatter(const Scene& S, const DMat& m, const Ray
     const V3 dir = unit(pdf_d);
     s.ray.d = dir;
     double v1 = 0.0;
-    if constexpr ((F & F_LIGHTS) != 0) v1 = S.lights >= 0 ? htbl_pdf_value<F, RT_LIGHT_DEPTH>(S, S.lights, h.p, dir) : 0.0;
+    if constexpr ((F & F_LIGHTS) != 0)
+      if (S.lights >= 0) v1 = htbl_pdf_value<F, RT_LIGHT_DEPTH>(S, S.lights, h.p, dir, prep(Ray{h.p, dir, 0.0}));
     const double cosine = dot(unit(dir), uvw.w);
     const double v2 = cosine <= 0 ? 0 : cosine / kPi;
     s.pdf = 0.5 * (v1 + v2);

@@ -30,6 +30,9 @@ RT_NODE_CUBOID, RT_NODE_TRANSLATE, RT_NODE_ROTATE = 6, 7, 8
 RT_NODE_CONSTANT_MEDIUM, RT_NODE_UNHITTABLE, RT_NODE_EXT = 9, 10, 11
 RT_RNG_EXACT, RT_RNG_PHILOX = 0, 1
 RT_FLAG_NAN_CULL = 1
+RT_FLAG_REFERENCE_CULL = 2
+MATH_OPS = {"div": 0, "div_exact": 1, "sqrt": 2, "sin": 3, "cos": 4, "atan": 5, "asin": 6, "log": 7, "pow": 8,
+            "ghc_atan2": 9, "tan": 10}
 
 XYPlane, XZPlane, YZPlane = 0, 1, 2
 XAxis, YAxis, ZAxis = 0, 1, 2
@@ -99,7 +102,7 @@ EXPORTED = [
     "rt_builder_finish", "rt_scene_named", "rt_camera_new", "rt_camera_named", "rt_write_ppm",
     "rt_device_count", "rt_create", "rt_destroy", "rt_upload_scene", "rt_render", "rt_shard_geometry",
     "rt_render_shard_async", "rt_assemble_async", "rt_assemble_linear_async", "rt_last_kernel_ms",
-    "rt_debug_closest_hits",
+    "rt_debug_closest_hits", "rt_debug_math",
 ]
 
 _lib = None
@@ -150,7 +153,8 @@ def lib() -> C.CDLL:
             "rt_assemble_async": (I, [C.c_void_p, P(rt_render_params), C.c_void_p, C.c_void_p, C.c_void_p]),
             "rt_assemble_linear_async": (I, [C.c_void_p, P(rt_render_params), C.c_void_p, C.c_void_p, C.c_void_p]),
             "rt_last_kernel_ms": (I, [C.c_void_p, P(D)]),
-            "rt_debug_closest_hits": (I, [C.c_void_p, P(D), I, D, D, U64, P(D)]),
+            "rt_debug_closest_hits": (I, [C.c_void_p, P(D), I, D, D, U64, C.c_uint32, P(D)]),
+            "rt_debug_math": (I, [C.c_void_p, I, P(D), P(D), I, P(D)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -436,12 +440,22 @@ class Context:
         _check(lib().rt_last_kernel_ms(self._h, C.byref(ms)), "rt_last_kernel_ms")
         return ms.value
 
-    def closest_hits(self, rays: np.ndarray, tmin: float, tmax: float, seed: int = 0) -> np.ndarray:
+    def closest_hits(self, rays: np.ndarray, tmin: float, tmax: float, seed: int = 0, flags: int = 0) -> np.ndarray:
         rays = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 7)
         out = np.zeros((rays.shape[0], 12), dtype=np.float64)
         P = C.POINTER
         _check(lib().rt_debug_closest_hits(self._h, rays.ctypes.data_as(P(C.c_double)), rays.shape[0], tmin, tmax,
-                                           seed, out.ctypes.data_as(P(C.c_double))), "rt_debug_closest_hits")
+                                           seed, flags, out.ctypes.data_as(P(C.c_double))), "rt_debug_closest_hits")
+        return out
+
+    def math(self, op: str, x: np.ndarray, y: Optional[np.ndarray] = None) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float64).reshape(-1)
+        y = np.ascontiguousarray(np.zeros_like(x) if y is None else y, dtype=np.float64).reshape(-1)
+        out = np.zeros_like(x)
+        P = C.POINTER
+        _check(lib().rt_debug_math(self._h, MATH_OPS[op], x.ctypes.data_as(P(C.c_double)),
+                                   y.ctypes.data_as(P(C.c_double)), x.size, out.ctypes.data_as(P(C.c_double))),
+               "rt_debug_math")
         return out
 
 

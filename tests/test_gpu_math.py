@@ -1,0 +1,82 @@
+"""Device numerics (GPU): the exact-division scheme must be bit-identical to IEEE division, and
+sqrt must be correctly rounded; fp64 transcendentals (OCML on the device, glibc in the oracle and
+in GHC) are measured in ulps — they are the only source of GPU/oracle divergence."""
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, dtype=np.float64).view(np.int64)
+
+
+def _adversarial(rng, n):
+    # mantissas of all ones / all zeros, powers of two, tiny/huge, zeros of both signs, inf, nan
+    m = rng.integers(0, 2 ** 52, n, dtype=np.int64)
+    special = np.array([0, 2 ** 52 - 1, 1, 2 ** 51, 2 ** 52 - 2], dtype=np.int64)
+    m[: n // 4] = special[rng.integers(0, special.size, n // 4)]
+    e = rng.integers(1023 - 60, 1023 + 60, n, dtype=np.int64)
+    e[: n // 50] = rng.integers(1, 2046, n // 50)
+    s = rng.integers(0, 2, n, dtype=np.int64) << 63
+    x = ((e << 52) | m | s).view(np.float64)
+    x[:8] = [0.0, -0.0, np.inf, -np.inf, np.nan, 5e-324, 1e-310, 1.7e308]
+    return x
+
+
+def test_div_exact_is_ieee_division(gpu_ctx):
+    rng = np.random.default_rng(1)
+    n = 1 << 22
+    for x, y in [(rng.normal(0, 100, n), rng.normal(0, 1, n)),
+                 (_adversarial(rng, n), _adversarial(rng, n)),
+                 (rng.uniform(-600, 600, n), rng.uniform(-1, 1, n) * 10.0 ** rng.integers(-20, 3, n))]:
+        ref = gpu_ctx.math("div", x, y)
+        got = gpu_ctx.math("div_exact", x, y)
+        with np.errstate(all="ignore"):
+            host = x / y
+        same = (_bits(got) == _bits(ref)) | (np.isnan(got) & np.isnan(ref))
+        assert same.all(), f"{(~same).sum()} mismatches, e.g. {x[~same][:3]} / {y[~same][:3]}"
+        same_h = (_bits(ref) == _bits(host)) | (np.isnan(ref) & np.isnan(host))
+        assert same_h.all(), "device IEEE division differs from host division"
+
+
+def test_sqrt_correctly_rounded(gpu_ctx):
+    rng = np.random.default_rng(2)
+    x = np.abs(np.concatenate([rng.normal(0, 1, 1 << 20), _adversarial(rng, 1 << 20)]))
+    got = gpu_ctx.math("sqrt", x)
+    host = np.sqrt(x)
+    same = (_bits(got) == _bits(host)) | (np.isnan(got) & np.isnan(host))
+    assert same.all()
+
+
+def _ulps(a, b):
+    ia, ib = _bits(a), _bits(b)
+    ia = np.where(ia < 0, np.int64(-2 ** 63) - ia, ia)
+    ib = np.where(ib < 0, np.int64(-2 ** 63) - ib, ib)
+    return np.abs(ia - ib)
+
+
+@pytest.mark.parametrize("op,fn,lo,hi", [("sin", math.sin, 0, 2 * math.pi), ("cos", math.cos, 0, 2 * math.pi),
+                                         ("sin", math.sin, -1e4, 1e4), ("atan", math.atan, -50, 50),
+                                         ("asin", math.asin, -1, 1), ("log", math.log, 0, 1),
+                                         ("tan", math.tan, 0, 1.5)])
+def test_transcendentals_within_two_ulps_of_glibc(gpu_ctx, op, fn, lo, hi):
+    rng = np.random.default_rng(3)
+    x = rng.uniform(lo, hi, 200000)
+    got = gpu_ctx.math(op, x)
+    host = np.array([fn(v) for v in x])
+    u = _ulps(got, host)
+    print(f"{op}[{lo},{hi}]: exact {float((u == 0).mean()):.4f}, max ulps {int(u.max())}")
+    assert u.max() <= 2
+
+
+def test_pow5_within_two_ulps(gpu_ctx):
+    rng = np.random.default_rng(4)
+    x = rng.uniform(0, 2, 200000)
+    got = gpu_ctx.math("pow", x, np.full_like(x, 5.0))
+    host = np.array([math.pow(v, 5.0) for v in x])
+    u = _ulps(got, host)
+    print(f"pow(x,5): exact {float((u == 0).mean()):.4f}, max ulps {int(u.max())}")
+    assert u.max() <= 2
