@@ -68,6 +68,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--nan-cull", action="store_true", help="RT_FLAG_NAN_CULL (output-identical)")
+    ap.add_argument("--reference-cull", action="store_true",
+                    help="RT_FLAG_REFERENCE_CULL: the reference's per-axis box test only (no joint slab filter)")
     ap.add_argument("--tile", type=int, default=16)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     ap.add_argument("--cpu-spp", type=int, default=4)
@@ -89,7 +91,8 @@ def main():
     cam = rtamd.camera(cfg["camera"], cfg["W"], cfg["H"])
     ctx = rtamd.Context(local)
     ctx.upload(scene)
-    flags = rtamd.RT_FLAG_NAN_CULL if args.nan_cull else 0
+    flags = (rtamd.RT_FLAG_NAN_CULL if args.nan_cull else 0) | (
+        rtamd.RT_FLAG_REFERENCE_CULL if args.reference_cull else 0)
     p = rtamd.make_params(cfg["W"], cfg["H"], cfg["spp"], cfg["depth"], rtamd.RT_RNG_PHILOX, seed=1024,
                           flags=flags, tile=args.tile, shard_rank=rank, shard_count=world)
     _, _, slab_px = rtamd.shard_geometry(p)
@@ -157,7 +160,8 @@ def main():
             "data": "synthetic (scene generated by the reference's makeRandomSceneBookOne from randGen 1024)",
             "config": {"workload": cfg["desc"], "width": cfg["W"], "height": cfg["H"], "spp": cfg["spp"],
                        "max_depth": cfg["depth"], "rng": "tier B Philox4x32-10 per (pixel, sample)",
-                       "nan_cull": bool(args.nan_cull), "tile": args.tile, "parallelism": f"tiles x{world}"},
+                       "nan_cull": bool(args.nan_cull), "box_cull": "reference" if args.reference_cull else "joint",
+                       "tile": args.tile, "parallelism": f"tiles x{world}"},
             "image_mean_rgb": [round(float(x), 3) for x in img.reshape(-1, 3).mean(0)],
         }
         cb = None
