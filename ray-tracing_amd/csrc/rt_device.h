@@ -55,16 +55,20 @@ struct Ray {
 };
 
 // Correctly rounded a / b from y = RN(1/b): two Markstein residual corrections (each residual
-// a - b*q is exact under FMA), then a range guard that falls back to the IEEE division whenever
-// the quotient is zero, tiny, huge or not finite. Bit-identical to `a / b` (tests/test_gpu_math).
+// a - b*q is exact under FMA when nothing under- or overflows), then a range guard that falls back
+// to the IEEE division unless |a|, |b| and |q| all lie in [2^-900, 2^900] (zero, tiny, huge and
+// non-finite operands included). Bit-identical to `a / b` (tests/test_gpu_math.py).
+__device__ __forceinline__ bool in_range(double x) {
+  const double ax = fabs(x);
+  return ax >= 0x1p-900 && ax <= 0x1p900;
+}
 __device__ __forceinline__ double div_exact(double a, double b, double y) {
   double q = a * y;
   double r = fma(-q, b, a);
   q = fma(r, y, q);
   r = fma(-q, b, a);
   q = fma(r, y, q);
-  const double aq = fabs(q);
-  if (!(aq >= 0x1p-900 && aq <= 0x1p900)) q = a / b;
+  if (!(in_range(a) && in_range(b) && in_range(q))) q = a / b;
   return q;
 }
 
@@ -78,10 +82,7 @@ struct RayX {
   double inva; // RN(1 / a)
   bool safe;
 };
-__device__ __forceinline__ bool div_ok(double b) {
-  const double ab = fabs(b);
-  return ab >= 0x1p-500 && ab <= 0x1p500;
-}
+__device__ __forceinline__ bool div_ok(double b) { return in_range(b); }
 __device__ __forceinline__ RayX prep(const Ray& r) {
   RayX x;
   x.o = r.o;

@@ -87,10 +87,8 @@ __device__ __forceinline__ double div_mk(double a, double b, double y) {
   r = fma(-q, b, a);
   return fma(r, y, q);
 }
-__device__ __forceinline__ bool q_ok(double q) {
-  const double aq = fabs(q);
-  return aq >= 0x1p-900 && aq <= 0x1p900;
-}
+// quotient and dividend both in the trusted range (divisors are covered by RayX::safe)
+__device__ __forceinline__ bool q_ok(double a, double q) { return in_range(a) && in_range(q); }
 
 // boxRayIntersect (Lib.hs:798-814): per axis, [max t0 t_min, min t1 t_max] must be non-empty,
 // with the reference's quotients (bit-exact) and GHC max/min. The reference never intersects the
@@ -104,9 +102,10 @@ __device__ __forceinline__ bool box_hit(const double* f, const RayX& r, double t
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     const double o = comp(r.o, a), d = comp(r.d, a), y = comp(r.inv, a);
-    q[2 * a] = div_mk(f[a] - o, d, y);
-    q[2 * a + 1] = div_mk(f[a + 3] - o, d, y);
-    good = good && q_ok(q[2 * a]) && q_ok(q[2 * a + 1]);
+    const double n0 = f[a] - o, n1 = f[a + 3] - o;
+    q[2 * a] = div_mk(n0, d, y);
+    q[2 * a + 1] = div_mk(n1, d, y);
+    good = good && q_ok(n0, q[2 * a]) && q_ok(n1, q[2 * a + 1]);
   }
   if (!good) {
 #pragma unroll
@@ -139,7 +138,7 @@ __device__ __forceinline__ bool rect_t(int plane, double i0, double i1, double j
   const int ii = plane == 2 ? 1 : 0, jj = plane == 0 ? 1 : 2, kk = plane == 0 ? 2 : (plane == 1 ? 1 : 0);
   const double num = k - comp(r.o, kk);
   double t = r.safe ? div_mk(num, comp(r.d, kk), comp(r.inv, kk)) : 0.0;
-  if (!r.safe || !q_ok(t)) t = num / comp(r.d, kk);
+  if (!r.safe || !q_ok(num, t)) t = num / comp(r.d, kk);
   if ((t < t_min) || (t > t_max)) return false;
   const double i = comp(r.o, ii) + t * comp(r.d, ii);
   const double j = comp(r.o, jj) + t * comp(r.d, jj);
@@ -180,7 +179,7 @@ __device__ __forceinline__ bool sphere_t(V3 sc, double sr, const RayX& r, double
   const double sd = sqrt(disc);
   const double n1 = (-b) - sd, n2 = (-b) + sd;
   double temp1 = div_mk(n1, a, r.inva), temp2 = div_mk(n2, a, r.inva);
-  if (!(r.safe && q_ok(temp1) && q_ok(temp2))) {
+  if (!(r.safe && q_ok(n1, temp1) && q_ok(n2, temp2))) {
     temp1 = n1 / a;
     temp2 = n2 / a;
   }

@@ -37,7 +37,8 @@ def test_div_exact_is_ieee_division(gpu_ctx):
         with np.errstate(all="ignore"):
             host = x / y
         same = (_bits(got) == _bits(ref)) | (np.isnan(got) & np.isnan(ref))
-        assert same.all(), f"{(~same).sum()} mismatches, e.g. {x[~same][:3]} / {y[~same][:3]}"
+        assert same.all(), (f"{(~same).sum()} mismatches, e.g. {x[~same][:3].tolist()} / {y[~same][:3].tolist()}"
+                            f" got {got[~same][:3].tolist()} want {ref[~same][:3].tolist()}")
         same_h = (_bits(ref) == _bits(host)) | (np.isnan(ref) & np.isnan(host))
         assert same_h.all(), "device IEEE division differs from host division"
 

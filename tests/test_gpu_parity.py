@@ -108,6 +108,12 @@ def test_closest_hits_bit_exact(gpu_ctx, name, flags):
     ref = pyoracle.closest_hits(sc, rays, 1e-4, np.inf, seed=3)
     assert got[:, 0].sum() > n // 4
     mism = np.any(got != ref, axis=1)
+    if mism.any():
+        i = np.where(mism)[0]
+        cols = np.where((got[i] != ref[i]).any(axis=0))[0]
+        print("mismatching rays", i[:5], "fields", cols)
+        for k in i[:3]:
+            print("ray", rays[k].tolist(), "\n gpu", got[k].tolist(), "\n ref", ref[k].tolist())
     assert mism.sum() == 0, f"{mism.sum()} of {n} rays differ"
 
 
