@@ -38,10 +38,14 @@ CONFIGS = {
 HBM_PEAK_GBS = 8000.0
 FP64_PEAK_TFLOPS = 78.6
 
-# Algorithmic record sizes (include/rt.h, DESIGN.md "Roofline"): bytes fetched per test.
-BYTES = {"box_tests": 64, "sphere_tests": 64, "rect_tests": 64, "other_prims": 64, "light_queries": 64}
-# fp64 operations per event (lower bound)
-FLOPS = {"box_tests": 12 + 6, "sphere_tests": 30, "rect_tests": 20, "scatters": 60, "draws": 15}
+# Algorithmic bytes per unit of device-counted work (DESIGN.md "Roofline"): every BVH box test,
+# leaf test and instance/medium test reads one 64-byte rt_node; every traced segment reads its
+# hit material + texture (24 + 48 B); every light-pdf evaluation reads the light record (64 B);
+# every pixel writes 3 bytes.
+BYTES = {"box_tests": 64, "prim_tests": 64, "other_tests": 64, "segments": 72, "light_pdfs": 64}
+# fp64 operations per unit (lower bound): box test 6 sub + 6 div + 6 min/max,
+# sphere test ~30, scatter/shading ~60 per segment.
+FLOPS = {"box_tests": 18, "prim_tests": 30, "other_tests": 30, "segments": 60}
 
 
 def log(*a):
@@ -74,6 +78,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     ap.add_argument("--cpu-spp", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-work", action="store_true", help="skip the counting-build pass")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -111,6 +116,9 @@ def main():
             src = slab
         if rank == 0:
             ctx.assemble_async(p, src.data_ptr(), image.data_ptr(), stream.cuda_stream)
+
+    # device-measured work of this exact launch (counting build, outside the timed region)
+    work = ctx.render_work(cam, p) if not args.no_work else None
 
     for i in range(args.warmup):
         step()
@@ -172,9 +180,9 @@ def main():
                   "sample": f"full {cfg['W']}x{cfg['H']} frame at {args.cpu_spp} spp (tier-B streams 0..{args.cpu_spp - 1}"
                             f" of every pixel), {dt:.1f} s, oracle/oracle.c fp64 glibc -O2 OpenMP"}
         out["cpu_baseline"] = cb
-        if counters:
-            n = max(1, counters["samples"])
-            per = {k: counters[k] / n for k in counters}
+        if work:
+            n = max(1, work["samples"])
+            per = {k: work[k] / n for k in work}
             bytes_per_sample = sum(BYTES[k] * per[k] for k in BYTES) + 3.0 / cfg["spp"]
             flops_per_sample = sum(FLOPS[k] * per[k] for k in FLOPS)
             samples_per_launch = samples_frame / world
@@ -184,13 +192,17 @@ def main():
                                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
                                "kernel_ms": round(kernel_avg, 3),
                                "bytes_per_sample": round(bytes_per_sample, 2),
-                               "note": "node-stream bytes (64 B per BVH box / primitive test) from oracle counters "
-                                       "on the cpu_baseline sample; the binding roof is FP64 VALU (see fp64)"}
+                               "note": "algorithmic scene-record bytes per sample, device-counted by the counting "
+                                       "build of the same launch; the binding roof is FP64 VALU (see fp64)"}
             out["fp64"] = {"achieved_tflops": round(fl, 3), "peak_tflops": FP64_PEAK_TFLOPS,
                            "frac": round(fl / FP64_PEAK_TFLOPS, 5), "flops_per_sample": round(flops_per_sample, 1)}
             out["work_per_sample"] = {k: round(v, 3) for k, v in per.items() if k != "samples"}
+            if counters:
+                out["work_per_sample_reference_cull"] = {k: round(v / max(1, counters["samples"]), 3)
+                                                         for k, v in counters.items() if k != "samples"}
         else:
             out["roofline"] = None
+        out["kernel_waves_per_simd"] = os.environ.get("RTAMD_WAVES", "default")
         print(json.dumps(out), flush=True)
     ctx.close()
     if world > 1:

@@ -321,6 +321,13 @@ int rt_assemble_async(rt_ctx* ctx, const rt_render_params* p, const uint8_t* d_s
 int rt_assemble_linear_async(rt_ctx* ctx, const rt_render_params* p, const double* d_slabs_linear,
                              double* d_image_linear, void* stream);
 
+/*
+ * Counting build of the tier-B render (same output, slower): device-measured work for the
+ * roofline. out_work = {segments traced, BVH box tests, leaf primitive tests, instance/medium
+ * tests, light-pdf evaluations, Philox blocks, samples, 0} for this shard.
+ */
+int rt_render_work(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* p, uint64_t out_work[8]);
+
 /* Timing of the last render launch on this ctx (HIP events on the launch stream), ms. */
 int rt_last_kernel_ms(rt_ctx* ctx, double* out_ms);
 

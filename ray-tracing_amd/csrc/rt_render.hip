@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -40,6 +41,7 @@ struct RenderArgs {
   long long work_total;  // slab pixels of this shard
   uint64_t seed;
   unsigned long long* counter;
+  unsigned long long* work;  // counting build: [segments, box, prim, other, light, blocks, samples]
   uint8_t* out_rgb;  // tier B: slab; tier A: image
   double* out_lin;
   uint64_t* gens;  // tier A: per-column (seed, gamma), updated in place
@@ -96,14 +98,14 @@ __device__ __forceinline__ void store_pixel(const RenderArgs& A, long long idx, 
 // path ends, with its contribution in `contrib` (rayColor, Lib.hs:1298-1333).
 template <unsigned F, class R>
 __device__ __forceinline__ bool segment(const RenderArgs& A, Ray& ray, V3& thr, int& depth, R& g, int* stk,
-                                        V3& contrib) {
+                                        V3& contrib, Cnt& cnt) {
   const Scene& S = A.S;
   if (depth <= 0) {  // d <= 0 -> black
     contrib = vmul(thr, v3(0.0, 0.0, 0.0));
     return true;
   }
   Hit h;
-  if (!traverse<F>(S, S.world, ray, kEps, INFINITY, h, g, stk, !(A.flags & RT_FLAG_REFERENCE_CULL))) {
+  if (!traverse<F>(S, S.world, ray, kEps, INFINITY, h, g, stk, !(A.flags & RT_FLAG_REFERENCE_CULL), cnt)) {
     contrib = vmul(thr, v3(S.bg[0], S.bg[1], S.bg[2]));
     return true;
   }
@@ -114,6 +116,7 @@ __device__ __forceinline__ bool segment(const RenderArgs& A, Ray& ray, V3& thr, 
     return true;
   }
   Scatter s;
+  if constexpr ((F & F_COUNT) != 0) cnt.light += (m.type == RT_MAT_LAMBERTIAN && S.lights >= 0);
   scatter<F>(S, m, ray, h, g, s);
   if (s.specular) {
     thr = vmul(thr, s.att);
@@ -129,8 +132,14 @@ __device__ __forceinline__ bool segment(const RenderArgs& A, Ray& ray, V3& thr, 
 }
 
 // ---------------------------------------------------------------- tier B: Philox per (pixel, sample)
-template <unsigned F>
-__global__ void __launch_bounds__(RT_BLOCK) render_philox(RenderArgs A) {
+// Wave-reduce a per-lane counter and add it once per wave.
+__device__ __forceinline__ void wave_add(unsigned long long* dst, unsigned long long v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off);
+  if ((threadIdx.x & 63) == 0) atomicAdd(dst, v);
+}
+
+template <unsigned F, int WAVES>
+__global__ void __launch_bounds__(RT_BLOCK, WAVES) render_philox(RenderArgs A) {
   __shared__ int stk_mem[RT_STACK * RT_BLOCK];
   int* stk = &stk_mem[threadIdx.x];
   const int lane = threadIdx.x & 63;
@@ -143,6 +152,8 @@ __global__ void __launch_bounds__(RT_BLOCK) render_philox(RenderArgs A) {
   V3 thr = v3(0, 0, 0), sum = v3(0, 0, 0);
   RngPhilox g;
   g.init(A.seed, 0, 0);
+  Cnt cnt{0, 0, 0, 0};
+  unsigned long long segs = 0, blocks = 0, samples = 0;
 
   for (;;) {
     // acquire pixels for idle lanes: one atomic per wave per round
@@ -180,7 +191,12 @@ __global__ void __launch_bounds__(RT_BLOCK) render_philox(RenderArgs A) {
       path = true;
     }
     V3 contrib;
-    if (segment<F>(A, ray, thr, depth, g, stk, contrib)) {
+    if constexpr ((F & F_COUNT) != 0) segs += depth > 0;
+    if (segment<F>(A, ray, thr, depth, g, stk, contrib, cnt)) {
+      if constexpr ((F & F_COUNT) != 0) {
+        blocks += g.pair;
+        ++samples;
+      }
       sum = sum + contrib;
       path = false;
       ++s;
@@ -190,6 +206,15 @@ __global__ void __launch_bounds__(RT_BLOCK) render_philox(RenderArgs A) {
         w = -1;
       }
     }
+  }
+  if constexpr ((F & F_COUNT) != 0) {  // lanes re-converge after the loop: one add per wave
+    wave_add(&A.work[0], segs);
+    wave_add(&A.work[1], cnt.box);
+    wave_add(&A.work[2], cnt.prim);
+    wave_add(&A.work[3], cnt.other);
+    wave_add(&A.work[4], cnt.light);
+    wave_add(&A.work[5], blocks);
+    wave_add(&A.work[6], samples);
   }
 }
 
@@ -219,7 +244,8 @@ __global__ void __launch_bounds__(RT_BLOCK) render_exact(RenderArgs A) {
       Ray ray = get_ray(A.cam, u, v, g);
       V3 thr = v3(1.0, 1.0, 1.0), contrib;
       int depth = A.max_depth;
-      while (!segment<F>(A, ray, thr, depth, g, stk, contrib)) {
+      Cnt cnt{0, 0, 0, 0};
+      while (!segment<F>(A, ray, thr, depth, g, stk, contrib, cnt)) {
       }
       sum = sum + contrib;
     }
@@ -260,7 +286,8 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
   g.init(seed, (uint32_t)i, 0);
   Hit h;
   double* o = out + 12 * (long long)i;
-  if (traverse<F_ALL | F_UV>(S, S.world, r, tmin, tmax, h, g, stk, joint != 0)) {
+  Cnt cnt{0, 0, 0, 0};
+  if (traverse<F_ALL | F_UV>(S, S.world, r, tmin, tmax, h, g, stk, joint != 0, cnt)) {
     o[0] = 1; o[1] = h.t;
     o[2] = h.p.x; o[3] = h.p.y; o[4] = h.p.z;
     o[5] = h.n.x; o[6] = h.n.y; o[7] = h.n.z;
@@ -501,11 +528,28 @@ unsigned variant_for(unsigned f) {
   if ((f & ~kVarCornell) == 0) return kVarCornell;
   return F_ALL;
 }
-const void* philox_variant(unsigned f) {
+// Occupancy target (waves per SIMD) of the render kernel; RTAMD_WAVES overrides (2, 3 or 4) for
+// A/B measurements.
+// Defaults: the largest occupancy that compiles without scratch spills (make resources).
+int waves_target(int dflt) {
+  const char* e = std::getenv("RTAMD_WAVES");
+  const int w = e ? std::atoi(e) : dflt;
+  return (w >= 1 && w <= 4) ? w : dflt;
+}
+template <unsigned F>
+const void* by_waves(int w) {
+  if (w == 2) return (const void*)render_philox<F, 2>;
+  if (w == 3) return (const void*)render_philox<F, 3>;
+  if (w == 4) return (const void*)render_philox<F, 4>;
+  return (const void*)render_philox<F, 1>;
+}
+const void* philox_variant(unsigned f, bool count) {
   switch (variant_for(f)) {
-    case kVarSpheres: return (const void*)render_philox<kVarSpheres>;
-    case kVarCornell: return (const void*)render_philox<kVarCornell>;
-    default: return (const void*)render_philox<F_ALL>;
+    case kVarSpheres:
+      return count ? (const void*)render_philox<kVarSpheres | F_COUNT, 1> : by_waves<kVarSpheres>(waves_target(3));
+    case kVarCornell:
+      return count ? (const void*)render_philox<kVarCornell | F_COUNT, 1> : by_waves<kVarCornell>(waves_target(1));
+    default: return count ? (const void*)render_philox<F_ALL | F_COUNT, 1> : (const void*)render_philox<F_ALL, 1>;
   }
 }
 const void* exact_variant(unsigned f) {
@@ -538,7 +582,7 @@ unsigned scene_features(const rt_scene_desc* d) {
 }
 
 int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int rank, int shards, uint8_t* d_rgb,
-                  double* d_lin, hipStream_t st) {
+                  double* d_lin, hipStream_t st, unsigned long long* d_work = nullptr) {
   RenderArgs A{};
   A.S = c->scene;
   A.cam = *cam;
@@ -555,10 +599,11 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   A.work_total = slab;
   A.seed = p->seed;
   A.counter = c->d_counter;
+  A.work = d_work;
   A.out_rgb = d_rgb;
   A.out_lin = d_lin;
   HIPCHK(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned long long), st));
-  const void* fn = philox_variant(c->features);
+  const void* fn = philox_variant(c->features, d_work != nullptr);
   int bpc = 1;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, RT_BLOCK, 0));
   const long long want = (slab + RT_BLOCK - 1) / RT_BLOCK;
@@ -594,7 +639,7 @@ int rt_create(int device, rt_ctx** out) {
   HIPCHK(hipGetDeviceProperties(&prop, device));
   c->cu_count = prop.multiProcessorCount;
   int bpc = 0;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, render_philox<F_ALL>, RT_BLOCK, 0));
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, render_philox<F_ALL, 1>, RT_BLOCK, 0));
   c->blocks_per_cu = bpc;
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIPCHK(hipEventCreate(&c->ev0));
@@ -795,6 +840,39 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, cons
   HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
   c->last_ms = ms;
   return RT_OK;
+}
+
+int rt_render_work(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, uint64_t out_work[8]) {
+  if (!c || !cam || !pin || !out_work) return invalid("null argument");
+  int rc = check_params(pin);
+  if (rc) return rc;
+  if (!c->has_scene) {
+    rt::set_error("rt_render_work: no scene uploaded");
+    return RT_E_STATE;
+  }
+  if (pin->rng_mode != RT_RNG_PHILOX) return invalid("rt_render_work: tier B only");
+  HIPCHK(hipSetDevice(c->device));
+  rt_render_params p = *pin;
+  const int shards = p.shard_count > 0 ? p.shard_count : 1;
+  int tile, tiles_x;
+  long long tt, ps, slab;
+  geometry(&p, tile, tiles_x, tt, ps, slab);
+  uint8_t* d_slab = nullptr;
+  unsigned long long* d_work = nullptr;
+  HIPCHK(hipMalloc((void**)&d_slab, (size_t)slab * 3));
+  HIPCHK(hipMalloc((void**)&d_work, sizeof(unsigned long long) * 8));
+  HIPCHK(hipMemsetAsync(d_work, 0, sizeof(unsigned long long) * 8, c->stream));
+  rc = launch_philox(c, cam, &p, p.shard_rank, shards, d_slab, nullptr, c->stream, d_work);
+  if (!rc) {
+    HIPCHK(hipStreamSynchronize(c->stream));
+    unsigned long long w[8];
+    HIPCHK(hipMemcpy(w, d_work, sizeof w, hipMemcpyDeviceToHost));
+    for (int i = 0; i < 8; ++i) out_work[i] = w[i];
+    out_work[7] = 0;
+  }
+  (void)hipFree(d_slab);
+  (void)hipFree(d_work);
+  return rc;
 }
 
 int rt_last_kernel_ms(rt_ctx* c, double* out_ms) {

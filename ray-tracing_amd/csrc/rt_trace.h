@@ -13,7 +13,13 @@ enum : unsigned {
   F_LIGHTS = 16u, // a lights tree (Lambertian light sampling / pdf)
   F_TEX = 32u,    // Checker / Perlin / Image textures (and sphere u, v)
   F_ALL = 63u,
-  F_UV = 64u      // always compute sphere (u, v) (debug queries)
+  F_UV = 64u,     // always compute sphere (u, v) (debug queries)
+  F_COUNT = 128u  // counting build: per-lane work counters (DESIGN.md "Roofline")
+};
+
+// Work counters of the counting build (F_COUNT); all zero-cost otherwise.
+struct Cnt {
+  unsigned box, prim, other, light;
 };
 
 // ------------------------------------------------------------------ textures (Lib.hs:441-513)
@@ -370,7 +376,7 @@ __device__ inline bool medium_hit(const Scene& S, const rt_node* n, const Ray& r
 // found inside it. `stk` is this lane's LDS stack (stride RT_BLOCK).
 template <unsigned F, class R>
 __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr, double t_min, double t_max,
-                                         Hit& best, R& g, int* stk, bool joint) {
+                                         Hit& best, R& g, int* stk, bool joint, Cnt& cnt) {
   const RayX wray = prep(wr);
   RayX ray = wray;
   int level = 0;
@@ -385,12 +391,14 @@ __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr
     const int tf = n->type;
     const int type = tf & RT_TYPE_MASK;
     if (type == RT_NODE_BVH) {
+      if constexpr ((F & F_COUNT) != 0) ++cnt.box;
       if (box_hit(n->f, ray, t_min, closest, joint)) {
         stk[(sp++) * RT_BLOCK] = n->b;
         node = n->a;
         continue;
       }
     } else if ((F & F_INST) && (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE)) {
+      if constexpr ((F & F_COUNT) != 0) ++cnt.other;
       if (tf & RT_CHAIN_PRIM) {
         Hit h;
         if (chain_hit<F>(S, node, plain(ray), t_min, closest, h)) {
@@ -408,6 +416,7 @@ __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr
         continue;
       }
     } else if ((F & F_MEDIA) && type == RT_NODE_CONSTANT_MEDIUM) {
+      if constexpr ((F & F_COUNT) != 0) ++cnt.other;
       Hit h;
       if (medium_hit<F>(S, n, plain(ray), t_min, closest, g, h)) {
         best = h;
@@ -417,6 +426,7 @@ __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr
         hitmask = (1u << level) - 1u;
       }
     } else {
+      if constexpr ((F & F_COUNT) != 0) ++cnt.prim;
       double t;
       int sub;
       if (prim_t<F>(S, n, ray, t_min, closest, t, sub)) {

@@ -102,7 +102,7 @@ EXPORTED = [
     "rt_builder_finish", "rt_scene_named", "rt_camera_new", "rt_camera_named", "rt_write_ppm",
     "rt_device_count", "rt_create", "rt_destroy", "rt_upload_scene", "rt_render", "rt_shard_geometry",
     "rt_render_shard_async", "rt_assemble_async", "rt_assemble_linear_async", "rt_last_kernel_ms",
-    "rt_debug_closest_hits", "rt_debug_math",
+    "rt_debug_closest_hits", "rt_debug_math", "rt_render_work",
 ]
 
 _lib = None
@@ -155,6 +155,7 @@ def lib() -> C.CDLL:
             "rt_last_kernel_ms": (I, [C.c_void_p, P(D)]),
             "rt_debug_closest_hits": (I, [C.c_void_p, P(D), I, D, D, U64, C.c_uint32, P(D)]),
             "rt_debug_math": (I, [C.c_void_p, I, P(D), P(D), I, P(D)]),
+            "rt_render_work": (I, [C.c_void_p, P(rt_camera), P(rt_render_params), P(U64)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -434,6 +435,14 @@ class Context:
     def assemble_linear_async(self, params, d_slabs: int, d_image: int, stream: int = 0):
         _check(lib().rt_assemble_linear_async(self._h, C.byref(params), C.c_void_p(d_slabs), C.c_void_p(d_image),
                                               C.c_void_p(stream or None)), "rt_assemble_linear_async")
+
+    WORK_FIELDS = ("segments", "box_tests", "prim_tests", "other_tests", "light_pdfs", "philox_blocks", "samples")
+
+    def render_work(self, cam, params) -> dict:
+        """Device-measured work of one tier-B render (counting build): totals per field."""
+        w = (C.c_uint64 * 8)()
+        _check(lib().rt_render_work(self._h, C.byref(cam), C.byref(params), w), "rt_render_work")
+        return dict(zip(self.WORK_FIELDS, [int(x) for x in w[:7]]))
 
     def last_kernel_ms(self) -> float:
         ms = C.c_double(0)
