@@ -30,6 +30,8 @@ CONFIGS = {
                desc="In-One-Weekend randomScene (makeRandomSceneBookOne) 1200x800x500spp d50"),
     "c3": dict(scene="cornell", camera="cornell", W=600, H=600, spp=1000, depth=50,
                desc="Cornell box (Rest-of-Your-Life) 600x600x1000spp d50"),
+    "c4": dict(scene="next_week_final", camera="next_week", W=800, H=800, spp=1000, depth=50, earth=True,
+               desc="The-Next-Week final scene (BVH, motion blur, Perlin, earthmap, media) 800x800x1000spp d50"),
     "c5": dict(scene="stress_spheres", camera="random_scene", W=3840, H=2160, spp=2000, depth=50, param=100000,
                desc="Stress: 100k random spheres 3840x2160x2000spp d50"),
 }
@@ -79,6 +81,8 @@ def main():
     ap.add_argument("--cpu-spp", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-work", action="store_true", help="skip the counting-build pass")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL over xGMI, default) or gloo (rehearsal: host-staged gather)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -86,13 +90,21 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    ndev = max(1, torch.cuda.device_count())
+    local = local % ndev  # one process per GPU; a rehearsal may put several ranks on one device
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     cfg = CONFIGS[args.config]
-    scene, _ = rtamd.make_scene(cfg["scene"], rtamd.randGen(1024), param=cfg.get("param", 0))
+    earth = None
+    if cfg.get("earth"):
+        earth = np.load(os.path.join(ROOT, "tests", "golden", "earthmap_rgb8.npz"))["rgb"]
+    scene, _ = rtamd.make_scene(cfg["scene"], rtamd.randGen(1024), param=cfg.get("param", 0), earth=earth)
     cam = rtamd.camera(cfg["camera"], cfg["W"], cfg["H"])
     ctx = rtamd.Context(local)
     ctx.upload(scene)
@@ -110,7 +122,13 @@ def main():
     def step():
         ctx.render_shard_async(cam, p, slab.data_ptr(), 0, stream.cuda_stream)
         if world > 1:
-            dist.all_gather_into_tensor(slabs, slab)
+            if args.dist_backend == "nccl":
+                dist.all_gather_into_tensor(slabs, slab)  # RCCL over xGMI
+            else:
+                host = slab.cpu()
+                parts = [torch.empty_like(host) for _ in range(world)]
+                dist.all_gather(parts, host)
+                slabs.copy_(torch.stack(parts))
             src = slabs
         else:
             src = slab
@@ -139,10 +157,11 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        rdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        km = torch.tensor([float(np.mean(kernel_ms))], dtype=torch.float64, device=dev)
+        km = torch.tensor([float(np.mean(kernel_ms))], dtype=torch.float64, device=rdev)
         dist.all_reduce(km, op=dist.ReduceOp.MAX)
         kernel_avg = float(km.item())
     else:
@@ -165,7 +184,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (scene generated by the reference's makeRandomSceneBookOne from randGen 1024)",
+            "data": f"synthetic (scene generated by the reference's {cfg['scene']} builder from randGen 1024)",
             "config": {"workload": cfg["desc"], "width": cfg["W"], "height": cfg["H"], "spp": cfg["spp"],
                        "max_depth": cfg["depth"], "rng": "tier B Philox4x32-10 per (pixel, sample)",
                        "nan_cull": bool(args.nan_cull), "box_cull": "reference" if args.reference_cull else "joint",
