@@ -102,7 +102,8 @@ __device__ __forceinline__ bool q_ok(double a, double q) { return in_range(a) &&
 // lower bounds < min of the upper bounds). That accepts a subset of the reference's boxes, so it
 // only prunes subtrees; what it prunes cannot hold a hit in [t_min, t_max] except exactly on a box
 // face (measure zero; tests/test_gpu_parity.py checks closest hits bit for bit).
-__device__ __forceinline__ bool box_hit(const double* f, const RayX& r, double t_min, double t_max, bool joint) {
+__device__ __forceinline__ bool box_hit_exact(const double* f, const RayX& r, double t_min, double t_max,
+                                              bool joint) {
   double q[6];
   bool good = r.safe;
 #pragma unroll
@@ -135,6 +136,32 @@ __device__ __forceinline__ bool box_hit(const double* f, const RayX& r, double t
     hmin = hi < hmin ? hi : hmin;
   }
   return ok && (!joint || hmin > lmax);
+}
+
+// The default (joint) test decided without divisions. When every quotient is finite and
+// non-NaN, (reference per-axis test) AND (joint test) is exactly L < U with
+// L = max(t_min, min(ta,tb) over axes) and U = min(t_max, max(ta,tb) over axes), and L and U are
+// each one of the exact quotients (or t_min / t_max). q' = n * RN(1/d) is within 2^-51 |q| of the
+// exact quotient q = RN(n / d), so L' and U' (same max/min over q') are within 2^-50 of L and U;
+// outside the band |U' - L'| <= 2^-48 (|L'| + |U'|) the sign of U' - L' is the sign of U - L.
+// Inside the band, or when any operand leaves the trusted range, the exact test decides.
+__device__ __forceinline__ bool box_hit(const double* f, const RayX& r, double t_min, double t_max, bool joint) {
+  if (!joint) return box_hit_exact(f, r, t_min, t_max, false);
+  double L = t_min, U = t_max;
+  bool good = r.safe;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const double o = comp(r.o, a), y = comp(r.inv, a);
+    const double n0 = f[a] - o, n1 = f[a + 3] - o;
+    const double ta = n0 * y, tb = n1 * y;
+    good = good && in_range(n0) && in_range(n1) && fabs(ta) <= 0x1p900 && fabs(tb) <= 0x1p900;
+    L = fmax(L, fmin(ta, tb));
+    U = fmin(U, fmax(ta, tb));
+  }
+  const double band = 0x1p-48 * (fabs(L) + fabs(U));
+  if (good && U - L > band) return true;
+  if (good && L - U > band) return false;
+  return box_hit_exact(f, r, t_min, t_max, true);
 }
 
 // rectHit's t (Lib.hs:1014-1028); plane 0 XY, 1 XZ, 2 YZ. Rejects only t < tmin or t > tmax
