@@ -97,15 +97,14 @@ __device__ __forceinline__ void store_pixel(const RenderArgs& A, long long idx, 
 // One path segment: closest hit, then emission/background or a scatter. Returns true when the
 // path ends, with its contribution in `contrib` (rayColor, Lib.hs:1298-1333).
 template <unsigned F, class R>
-__device__ __forceinline__ bool segment(const RenderArgs& A, Ray& ray, V3& thr, int& depth, R& g, int* stk,
-                                        V3& contrib, Cnt& cnt) {
-  const Scene& S = A.S;
+__device__ __forceinline__ bool segment(const RenderArgs& A, const Scene& S, Ray& ray, V3& thr, int& depth, R& g,
+                                        int* stk, V3& contrib, Cnt& cnt, int stride = RT_BLOCK) {
   if (depth <= 0) {  // d <= 0 -> black
     contrib = vmul(thr, v3(0.0, 0.0, 0.0));
     return true;
   }
   Hit h;
-  if (!traverse<F>(S, S.world, ray, kEps, INFINITY, h, g, stk, !(A.flags & RT_FLAG_REFERENCE_CULL), cnt)) {
+  if (!traverse<F>(S, S.world, ray, kEps, INFINITY, h, g, stk, !(A.flags & RT_FLAG_REFERENCE_CULL), cnt, stride)) {
     contrib = vmul(thr, v3(S.bg[0], S.bg[1], S.bg[2]));
     return true;
   }
@@ -138,10 +137,9 @@ __device__ __forceinline__ void wave_add(unsigned long long* dst, unsigned long 
   if ((threadIdx.x & 63) == 0) atomicAdd(dst, v);
 }
 
-template <unsigned F, int WAVES>
-__global__ void __launch_bounds__(RT_BLOCK, WAVES) render_philox(RenderArgs A) {
-  __shared__ int stk_mem[RT_STACK * RT_BLOCK];
-  int* stk = &stk_mem[threadIdx.x];
+// The persistent tier-B loop, shared by the global-memory and LDS-staged kernels.
+template <unsigned F>
+__device__ __forceinline__ void philox_loop(const RenderArgs& A, const Scene& S, int* stk, int stride) {
   const int lane = threadIdx.x & 63;
   const unsigned long long lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
@@ -192,7 +190,7 @@ __global__ void __launch_bounds__(RT_BLOCK, WAVES) render_philox(RenderArgs A) {
     }
     V3 contrib;
     if constexpr ((F & F_COUNT) != 0) segs += depth > 0;
-    if (segment<F>(A, ray, thr, depth, g, stk, contrib, cnt)) {
+    if (segment<F>(A, S, ray, thr, depth, g, stk, contrib, cnt, stride)) {
       if constexpr ((F & F_COUNT) != 0) {
         blocks += g.pair;
         ++samples;
@@ -216,6 +214,33 @@ __global__ void __launch_bounds__(RT_BLOCK, WAVES) render_philox(RenderArgs A) {
     wave_add(&A.work[5], blocks);
     wave_add(&A.work[6], samples);
   }
+}
+
+template <unsigned F, int WAVES>
+__global__ void __launch_bounds__(RT_BLOCK, WAVES) render_philox(RenderArgs A) {
+  __shared__ int stk_mem[RT_STACK * RT_BLOCK];
+  philox_loop<F>(A, A.S, &stk_mem[threadIdx.x], RT_BLOCK);
+}
+
+// LDS-staged variant: one workgroup of WAVES*4 waves per CU; the whole node array is copied
+// into LDS once, ahead of the traversal stack, so every node fetch of the traversal's
+// dependent chain is an LDS read (~64 cycles) instead of an L2 hit (~200-500 cycles).
+template <unsigned F, int WAVES>
+__global__ void __launch_bounds__(WAVES * 256, WAVES) render_philox_lds(RenderArgs A, int n_nodes, int stack_entries) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  rt_node* nodes = reinterpret_cast<rt_node*>(lds);
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(A.S.nodes);
+    uint4* dst = reinterpret_cast<uint4*>(lds);
+    const int n16 = n_nodes * (int)(sizeof(rt_node) / 16);
+    for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  Scene S = A.S;
+  S.nodes = nodes;
+  int* stk = reinterpret_cast<int*>(lds + (size_t)n_nodes * sizeof(rt_node)) + threadIdx.x;
+  (void)stack_entries;
+  philox_loop<F>(A, S, stk, WAVES * 256);
 }
 
 // ---------------------------------------------------------------- tier A: the reference's stream
@@ -245,7 +270,7 @@ __global__ void __launch_bounds__(RT_BLOCK) render_exact(RenderArgs A) {
       V3 thr = v3(1.0, 1.0, 1.0), contrib;
       int depth = A.max_depth;
       Cnt cnt{0, 0, 0, 0};
-      while (!segment<F>(A, ray, thr, depth, g, stk, contrib, cnt)) {
+      while (!segment<F>(A, A.S, ray, thr, depth, g, stk, contrib, cnt)) {
       }
       sum = sum + contrib;
     }
@@ -337,6 +362,8 @@ struct rt_ctx {
   uint8_t* d_pool = nullptr;
   Scene scene{};
   unsigned features = 0;
+  int n_nodes = 0;
+  int stack_need = 0;  // deepest traversal stack the world tree needs (entries)
   bool has_scene = false;
   unsigned long long* d_counter = nullptr;
   double last_ms = 0.0;
@@ -552,6 +579,14 @@ const void* philox_variant(unsigned f, bool count) {
     default: return count ? (const void*)render_philox<F_ALL | F_COUNT, 1> : (const void*)render_philox<F_ALL, 1>;
   }
 }
+const void* lds_variant(unsigned var, int waves) {
+  if (var == kVarSpheres) {
+    if (waves == 2) return (const void*)render_philox_lds<kVarSpheres, 2>;
+    if (waves == 4) return (const void*)render_philox_lds<kVarSpheres, 4>;
+    return (const void*)render_philox_lds<kVarSpheres, 3>;
+  }
+  return (const void*)render_philox_lds<kVarCornell, 1>;
+}
 const void* exact_variant(unsigned f) {
   switch (variant_for(f)) {
     case kVarSpheres: return (const void*)render_exact<kVarSpheres>;
@@ -603,6 +638,27 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   A.out_rgb = d_rgb;
   A.out_lin = d_lin;
   HIPCHK(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned long long), st));
+  // LDS-staged kernel when the node array plus the traversal stack fit one CU's 160 KiB
+  // (RTAMD_LDS=0 disables it for A/B runs).
+  const char* lds_env = std::getenv("RTAMD_LDS");
+  const bool lds_ok = !(lds_env && lds_env[0] == '0') && d_work == nullptr;
+  const unsigned var = variant_for(c->features);
+  if (lds_ok && (var == kVarSpheres || var == kVarCornell)) {
+    const int waves = var == kVarSpheres ? waves_target(3) : 1;
+    const int block = waves * 256;
+    const int entries = c->stack_need + 2;
+    const size_t bytes = (size_t)c->n_nodes * sizeof(rt_node) + (size_t)entries * block * sizeof(int);
+    if (bytes <= 160 * 1024) {
+      const void* fn = lds_variant(var, waves);
+      HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+      int n_nodes = c->n_nodes;
+      void* args[] = {&A, &n_nodes, (void*)&entries};
+      HIPCHK(hipEventRecord(c->ev0, st));
+      HIPCHK(hipLaunchKernel(fn, dim3(c->cu_count), dim3(block), args, bytes, st));
+      HIPCHK(hipEventRecord(c->ev1, st));
+      return RT_OK;
+    }
+  }
   const void* fn = philox_variant(c->features, d_work != nullptr);
   int bpc = 1;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, RT_BLOCK, 0));
@@ -711,6 +767,8 @@ int rt_upload_scene(rt_ctx* c, const rt_scene_desc* d) {
   S.lights = d->lights_root;
   for (int i = 0; i < 3; ++i) S.bg[i] = d->background[i];
   c->features = scene_features(d);
+  c->n_nodes = d->n_nodes;
+  c->stack_need = v.stack_need[d->world_root];
   c->has_scene = true;
   return RT_OK;
 }

@@ -400,10 +400,10 @@ __device__ inline bool medium_hit(const Scene& S, const rt_node* n, const Ray& r
 // records only (t, node, face); its record is built once at the end from the same ray with the
 // same operations. Instances whose subtree is not a primitive chain open a frame (a tagged stack
 // entry); the frame's rewrite of the hit is applied when the frame closes if the closest hit was
-// found inside it. `stk` is this lane's LDS stack (stride RT_BLOCK).
+// found inside it. `stk` is this lane's LDS stack (entries `stride` ints apart).
 template <unsigned F, class R>
 __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr, double t_min, double t_max,
-                                         Hit& best, R& g, int* stk, bool joint, Cnt& cnt) {
+                                         Hit& best, R& g, int* stk, bool joint, Cnt& cnt, int stride = RT_BLOCK) {
   const RayX wray = prep(wr);
   RayX ray = wray;
   int level = 0;
@@ -420,7 +420,7 @@ __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr
     if (type == RT_NODE_BVH) {
       if constexpr ((F & F_COUNT) != 0) ++cnt.box;
       if (box_hit(n->f, ray, t_min, closest, joint)) {
-        stk[(sp++) * RT_BLOCK] = n->b;
+        stk[(sp++) * stride] = n->b;
         node = n->a;
         continue;
       }
@@ -436,7 +436,7 @@ __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr
           hitmask = (1u << level) - 1u;
         }
       } else {
-        stk[(sp++) * RT_BLOCK] = RT_FRAME | node;
+        stk[(sp++) * stride] = RT_FRAME | node;
         ray = prep(enter_instance(n, plain(ray)));
         ++level;
         node = n->a;
@@ -475,7 +475,7 @@ __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr
         if (!best_full) prim_record<F>(S, &S.nodes[best_node], best_sub, wr, closest, best);
         return true;
       }
-      const int e = stk[(--sp) * RT_BLOCK];
+      const int e = stk[(--sp) * stride];
       if (!(F & F_INST) || !(e & RT_FRAME)) {
         node = e;
         break;
@@ -488,7 +488,7 @@ __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr
       --level;
       Ray pr = wr;  // rebuild the parent's ray from the world ray through the still-open frames
       for (int k = 0; k < sp; ++k) {
-        const int f = stk[k * RT_BLOCK];
+        const int f = stk[k * stride];
         if (f & RT_FRAME) pr = enter_instance(&S.nodes[f & ~RT_FRAME], pr);
       }
       ray = prep(pr);
