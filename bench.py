@@ -201,6 +201,7 @@ def main():
         out["cpu_baseline"] = cb
         if work:
             n = max(1, work["samples"])
+            out["phase_split"] = {k: round(v, 4) for k, v in work.pop("phase_split").items()}
             per = {k: work[k] / n for k in work}
             bytes_per_sample = sum(BYTES[k] * per[k] for k in BYTES) + 3.0 / cfg["spp"]
             flops_per_sample = sum(FLOPS[k] * per[k] for k in FLOPS)

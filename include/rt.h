@@ -323,10 +323,12 @@ int rt_assemble_linear_async(rt_ctx* ctx, const rt_render_params* p, const doubl
 
 /*
  * Counting build of the tier-B render (same output, slower): device-measured work for the
- * roofline. out_work = {segments traced, BVH box tests, leaf primitive tests, instance/medium
- * tests, light-pdf evaluations, Philox blocks, samples, 0} for this shard.
+ * roofline. out_work[0..6] = {segments traced, BVH box tests, leaf primitive tests,
+ * instance/medium tests, light-pdf evaluations, Philox blocks, samples} for this shard;
+ * out_work[8..10] = wave time (s_memtime ticks, summed over waves) spent acquiring work and
+ * starting samples / traversing / shading; the rest 0.
  */
-int rt_render_work(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* p, uint64_t out_work[8]);
+int rt_render_work(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* p, uint64_t out_work[16]);
 
 /* Timing of the last render launch on this ctx (HIP events on the launch stream), ms. */
 int rt_last_kernel_ms(rt_ctx* ctx, double* out_ms);

@@ -32,6 +32,16 @@ using namespace rtd;
 
 namespace {
 
+// Wave-level timestamp for the counting build's phase split (MI355X_MICROARCH.md / HIP guide
+// "In-kernel stamps": one asm statement with its own lgkmcnt wait, fenced by sched barriers).
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
 struct RenderArgs {
   Scene S;
   rt_camera cam;
@@ -98,13 +108,17 @@ __device__ __forceinline__ void store_pixel(const RenderArgs& A, long long idx, 
 // path ends, with its contribution in `contrib` (rayColor, Lib.hs:1298-1333).
 template <unsigned F, class R>
 __device__ __forceinline__ bool segment(const RenderArgs& A, const Scene& S, Ray& ray, V3& thr, int& depth, R& g,
-                                        int* stk, V3& contrib, Cnt& cnt, int stride = RT_BLOCK) {
+                                        int* stk, V3& contrib, Cnt& cnt, int stride = RT_BLOCK,
+                                        unsigned long long* t_trav = nullptr) {
   if (depth <= 0) {  // d <= 0 -> black
     contrib = vmul(thr, v3(0.0, 0.0, 0.0));
     return true;
   }
   Hit h;
-  if (!traverse<F>(S, S.world, ray, kEps, INFINITY, h, g, stk, !(A.flags & RT_FLAG_REFERENCE_CULL), cnt, stride)) {
+  const bool got = traverse<F>(S, S.world, ray, kEps, INFINITY, h, g, stk, !(A.flags & RT_FLAG_REFERENCE_CULL), cnt,
+                               stride);
+  if constexpr ((F & F_COUNT) != 0) *t_trav = stamp();
+  if (!got) {
     contrib = vmul(thr, v3(S.bg[0], S.bg[1], S.bg[2]));
     return true;
   }
@@ -152,8 +166,10 @@ __device__ __forceinline__ void philox_loop(const RenderArgs& A, const Scene& S,
   g.init(A.seed, 0, 0);
   Cnt cnt{0, 0, 0, 0};
   unsigned long long segs = 0, blocks = 0, samples = 0;
+  unsigned long long ph_acq = 0, ph_trav = 0, ph_shade = 0, s0 = 0, s1 = 0, s2 = 0;
 
   for (;;) {
+    if constexpr ((F & F_COUNT) != 0) s0 = stamp();
     // acquire pixels for idle lanes: one atomic per wave per round
     for (;;) {
       const bool need = (w < 0) && !done;
@@ -189,8 +205,19 @@ __device__ __forceinline__ void philox_loop(const RenderArgs& A, const Scene& S,
       path = true;
     }
     V3 contrib;
-    if constexpr ((F & F_COUNT) != 0) segs += depth > 0;
-    if (segment<F>(A, S, ray, thr, depth, g, stk, contrib, cnt, stride)) {
+    if constexpr ((F & F_COUNT) != 0) {
+      segs += depth > 0;
+      s1 = stamp();
+      s2 = s1;
+    }
+    const bool ended = segment<F>(A, S, ray, thr, depth, g, stk, contrib, cnt, stride, &s2);
+    if constexpr ((F & F_COUNT) != 0) {
+      const unsigned long long s3 = stamp();
+      ph_acq += s1 - s0;
+      ph_trav += s2 - s1;
+      ph_shade += s3 - s2;
+    }
+    if (ended) {
       if constexpr ((F & F_COUNT) != 0) {
         blocks += g.pair;
         ++samples;
@@ -213,6 +240,11 @@ __device__ __forceinline__ void philox_loop(const RenderArgs& A, const Scene& S,
     wave_add(&A.work[4], cnt.light);
     wave_add(&A.work[5], blocks);
     wave_add(&A.work[6], samples);
+    if ((threadIdx.x & 63) == 0) {  // wave-uniform phase times (s_memtime ticks)
+      atomicAdd(&A.work[8], ph_acq);
+      atomicAdd(&A.work[9], ph_trav);
+      atomicAdd(&A.work[10], ph_shade);
+    }
   }
 }
 
@@ -900,7 +932,7 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, cons
   return RT_OK;
 }
 
-int rt_render_work(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, uint64_t out_work[8]) {
+int rt_render_work(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, uint64_t out_work[16]) {
   if (!c || !cam || !pin || !out_work) return invalid("null argument");
   int rc = check_params(pin);
   if (rc) return rc;
@@ -918,15 +950,14 @@ int rt_render_work(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin,
   uint8_t* d_slab = nullptr;
   unsigned long long* d_work = nullptr;
   HIPCHK(hipMalloc((void**)&d_slab, (size_t)slab * 3));
-  HIPCHK(hipMalloc((void**)&d_work, sizeof(unsigned long long) * 8));
-  HIPCHK(hipMemsetAsync(d_work, 0, sizeof(unsigned long long) * 8, c->stream));
+  HIPCHK(hipMalloc((void**)&d_work, sizeof(unsigned long long) * 16));
+  HIPCHK(hipMemsetAsync(d_work, 0, sizeof(unsigned long long) * 16, c->stream));
   rc = launch_philox(c, cam, &p, p.shard_rank, shards, d_slab, nullptr, c->stream, d_work);
   if (!rc) {
     HIPCHK(hipStreamSynchronize(c->stream));
-    unsigned long long w[8];
+    unsigned long long w[16];
     HIPCHK(hipMemcpy(w, d_work, sizeof w, hipMemcpyDeviceToHost));
-    for (int i = 0; i < 8; ++i) out_work[i] = w[i];
-    out_work[7] = 0;
+    for (int i = 0; i < 16; ++i) out_work[i] = w[i];
   }
   (void)hipFree(d_slab);
   (void)hipFree(d_work);

@@ -440,9 +440,12 @@ class Context:
 
     def render_work(self, cam, params) -> dict:
         """Device-measured work of one tier-B render (counting build): totals per field."""
-        w = (C.c_uint64 * 8)()
+        w = (C.c_uint64 * 16)()
         _check(lib().rt_render_work(self._h, C.byref(cam), C.byref(params), w), "rt_render_work")
-        return dict(zip(self.WORK_FIELDS, [int(x) for x in w[:7]]))
+        out = dict(zip(self.WORK_FIELDS, [int(x) for x in w[:7]]))
+        tot = max(1, int(w[8]) + int(w[9]) + int(w[10]))
+        out["phase_split"] = {"acquire_camera": int(w[8]) / tot, "traverse": int(w[9]) / tot, "shade": int(w[10]) / tot}
+        return out
 
     def last_kernel_ms(self) -> float:
         ms = C.c_double(0)
