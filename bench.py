@@ -76,6 +76,8 @@ def main():
     ap.add_argument("--nan-cull", action="store_true", help="RT_FLAG_NAN_CULL (output-identical)")
     ap.add_argument("--reference-cull", action="store_true",
                     help="RT_FLAG_REFERENCE_CULL: the reference's per-axis box test only (no joint slab filter)")
+    ap.add_argument("--reference-bvh", action="store_true",
+                    help="traverse the reference's makeBVH world tree (default: SAH rebuild over the same leaves)")
     ap.add_argument("--tile", type=int, default=16)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     ap.add_argument("--cpu-spp", type=int, default=4)
@@ -107,7 +109,7 @@ def main():
     scene, _ = rtamd.make_scene(cfg["scene"], rtamd.randGen(1024), param=cfg.get("param", 0), earth=earth)
     cam = rtamd.camera(cfg["camera"], cfg["W"], cfg["H"])
     ctx = rtamd.Context(local)
-    ctx.upload(scene)
+    ctx.upload(scene, reference_bvh=args.reference_bvh)
     flags = (rtamd.RT_FLAG_NAN_CULL if args.nan_cull else 0) | (
         rtamd.RT_FLAG_REFERENCE_CULL if args.reference_cull else 0)
     p = rtamd.make_params(cfg["W"], cfg["H"], cfg["spp"], cfg["depth"], rtamd.RT_RNG_PHILOX, seed=1024,
@@ -188,6 +190,7 @@ def main():
             "config": {"workload": cfg["desc"], "width": cfg["W"], "height": cfg["H"], "spp": cfg["spp"],
                        "max_depth": cfg["depth"], "rng": "tier B Philox4x32-10 per (pixel, sample)",
                        "nan_cull": bool(args.nan_cull), "box_cull": "reference" if args.reference_cull else "joint",
+                       "world_bvh": "reference makeBVH" if args.reference_bvh else "SAH rebuild (media-free worlds)",
                        "tile": args.tile, "parallelism": f"tiles x{world}"},
             "image_mean_rgb": [round(float(x), 3) for x in img.reshape(-1, 3).mean(0)],
         }

@@ -286,8 +286,16 @@ int rt_device_count(int* out);
 /* Bind one HIP device (one process per GPU). */
 int rt_create(int device, rt_ctx** out);
 void rt_destroy(rt_ctx* ctx);
-/* Copy a scene to device memory (caller-owned desc; arrays are copied). Validates it. */
+/* Copy a scene to device memory (caller-owned desc; arrays are copied). Validates it.
+ * By default a world tree without ConstantMedium is re-bounded by a binned-SAH BVH over the same
+ * leaves for traversal (closest hits are tree-independent except for exact ties);
+ * the lights tree is always the caller's. */
 int rt_upload_scene(rt_ctx* ctx, const rt_scene_desc* desc);
+#define RT_UPLOAD_REFERENCE_BVH 1u /* traverse the caller's (makeBVH's) world tree as is */
+int rt_upload_scene_ex(rt_ctx* ctx, const rt_scene_desc* desc, uint32_t flags);
+/* The rebuild rt_upload_scene applies, on the host: the node array with the new world BVH
+ * appended (out_nodes NULL: size query) and the new world root (== the old one if ineligible). */
+int rt_rebuild_bvh(const rt_scene_desc* desc, rt_node* out_nodes, int capacity, int* out_n, int* out_root);
 
 /*
  * Blocking full-image render (replaces runRender, src/Lib.hs:1491).

@@ -1,0 +1,279 @@
+// rt_bvh.cpp — host-side world-BVH rebuild (binned SAH) for the device traversal.
+//
+// The reference's makeBVH (src/Lib.hs:941-961) splits at the median of a random axis after a
+// stable sort by box minimum, so boxes become long strips and a huge primitive (the r = 1000
+// ground sphere of the book-one scenes) sits on one spine at every level. For a world tree with
+// no ConstantMedium in it, the closest hit over the tree (hit, src/Lib.hs:970-1109) does not
+// depend on the tree's shape except for exact ties (two primitives at bit-identical t): every
+// leaf's own hit test is unchanged, and boxes only cull. So the device may traverse a better
+// tree over the SAME leaves (spheres, rects, cuboids, instance sub-DAGs, moving spheres, each
+// bounded exactly as boundingBox bounds it). Media keep the reference tree: the order in which
+// media are visited fixes their RNG draws. The lights tree is never touched (its BVH sizes weight
+// htblPdfValue / htblRandom, src/Lib.hs:694-723).
+#include <algorithm>
+#include <cmath>
+#include <functional>
+#include <vector>
+
+#include "rt.h"
+#include "rt_internal.h"
+
+namespace rt {
+
+namespace {
+
+constexpr double kEps = 0.0001;
+inline double gmax(double x, double y) { return x <= y ? y : x; }
+inline double gmin(double x, double y) { return x <= y ? x : y; }
+
+struct Builder {
+  std::vector<rt_node>& nodes;
+  std::vector<Box> boxes;  // per leaf
+  std::vector<int> leaf_ids;
+  std::vector<double> cx[3];
+
+  int emit_bvh(int l, int r, const Box& b, int size) {
+    rt_node n{};
+    for (int i = 0; i < 3; ++i) {
+      n.f[i] = b.mn[i];
+      n.f[3 + i] = b.mx[i];
+    }
+    n.type = RT_NODE_BVH;
+    n.a = l;
+    n.b = r;
+    n.c = size;
+    nodes.push_back(n);
+    return (int)nodes.size() - 1;
+  }
+
+  static Box merge(const Box& a, const Box& b) {
+    Box o;
+    for (int i = 0; i < 3; ++i) {
+      o.mn[i] = std::min(a.mn[i], b.mn[i]);
+      o.mx[i] = std::max(a.mx[i], b.mx[i]);
+    }
+    return o;
+  }
+  static double area(const Box& b) {
+    const double dx = b.mx[0] - b.mn[0], dy = b.mx[1] - b.mn[1], dz = b.mx[2] - b.mn[2];
+    return 2.0 * (dx * dy + dy * dz + dz * dx);
+  }
+
+  // Build over items[lo, hi); returns the node id and its box.
+  int build(std::vector<int>& items, int lo, int hi, Box& out) {
+    const int n = hi - lo;
+    if (n == 1) {
+      out = boxes[items[lo]];
+      return leaf_ids[items[lo]];
+    }
+    Box bb = boxes[items[lo]], cb;
+    for (int a = 0; a < 3; ++a) cb.mn[a] = cb.mx[a] = cx[a][items[lo]];
+    for (int i = lo + 1; i < hi; ++i) {
+      bb = merge(bb, boxes[items[i]]);
+      for (int a = 0; a < 3; ++a) {
+        cb.mn[a] = std::min(cb.mn[a], cx[a][items[i]]);
+        cb.mx[a] = std::max(cb.mx[a], cx[a][items[i]]);
+      }
+    }
+    int mid = lo + n / 2;
+    if (n > 2) {
+      constexpr int kBins = 16;
+      double best = INFINITY;
+      int best_axis = -1, best_bin = 0;
+      for (int a = 0; a < 3; ++a) {
+        const double ext = cb.mx[a] - cb.mn[a];
+        if (!(ext > 0)) continue;
+        Box bin_box[kBins];
+        int bin_cnt[kBins] = {0};
+        for (int i = lo; i < hi; ++i) {
+          int k = (int)((cx[a][items[i]] - cb.mn[a]) / ext * kBins);
+          k = std::min(kBins - 1, std::max(0, k));
+          bin_box[k] = bin_cnt[k] ? merge(bin_box[k], boxes[items[i]]) : boxes[items[i]];
+          ++bin_cnt[k];
+        }
+        // sweep: cost(split after bin k) = A_left * N_left + A_right * N_right
+        double right_area[kBins];
+        int right_cnt[kBins];
+        Box acc;
+        int cnt = 0;
+        for (int k = kBins - 1; k > 0; --k) {
+          if (bin_cnt[k]) {
+            acc = cnt ? merge(acc, bin_box[k]) : bin_box[k];
+            cnt += bin_cnt[k];
+          }
+          right_area[k] = cnt ? area(acc) : 0.0;
+          right_cnt[k] = cnt;
+        }
+        cnt = 0;
+        for (int k = 0; k < kBins - 1; ++k) {
+          if (bin_cnt[k]) {
+            acc = cnt ? merge(acc, bin_box[k]) : bin_box[k];
+            cnt += bin_cnt[k];
+          }
+          if (!cnt || !right_cnt[k + 1]) continue;
+          const double cost = area(acc) * cnt + right_area[k + 1] * right_cnt[k + 1];
+          if (cost < best) {
+            best = cost;
+            best_axis = a;
+            best_bin = k;
+          }
+        }
+      }
+      if (best_axis >= 0) {
+        const int a = best_axis;
+        const double ext = cb.mx[a] - cb.mn[a];
+        auto it = std::stable_partition(items.begin() + lo, items.begin() + hi, [&](int i) {
+          int k = (int)((cx[a][i] - cb.mn[a]) / ext * kBins);
+          k = std::min(kBins - 1, std::max(0, k));
+          return k <= best_bin;
+        });
+        mid = (int)(it - items.begin());
+        if (mid == lo || mid == hi) mid = lo + n / 2;
+      }
+    }
+    Box bl, br;
+    const int l = build(items, lo, mid, bl);
+    const int r = build(items, mid, hi, br);
+    out = merge(bl, br);
+    return emit_bvh(l, r, out, n);
+  }
+};
+
+}  // namespace
+
+// boundingBox (src/Lib.hs:905-927) over the flat node array (Rotate's box re-derived with its
+// 3x3x3 corner fold, exactly as `rotate` computes it at construction).
+bool flat_box(const std::vector<rt_node>& nodes, int id, Box* out) {
+  const rt_node& n = nodes[id];
+  switch (n.type) {
+    case RT_NODE_SPHERE:
+      for (int i = 0; i < 3; ++i) { out->mn[i] = n.f[i] - n.f[3]; out->mx[i] = n.f[i] + n.f[3]; }
+      return true;
+    case RT_NODE_MOVING_SPHERE: {
+      const double r = nodes[id + 1].f[3];
+      for (int i = 0; i < 3; ++i) {
+        out->mn[i] = gmin(n.f[i] - r, n.f[3 + i] - r);
+        out->mx[i] = gmax(n.f[i] + r, n.f[3 + i] + r);
+      }
+      return true;
+    }
+    case RT_NODE_RECT_XY:
+      out->mn[0] = n.f[0]; out->mn[1] = n.f[2]; out->mn[2] = n.f[4] - kEps;
+      out->mx[0] = n.f[1]; out->mx[1] = n.f[3]; out->mx[2] = n.f[4] + kEps;
+      return true;
+    case RT_NODE_RECT_XZ:
+      out->mn[0] = n.f[0]; out->mn[1] = n.f[4] - kEps; out->mn[2] = n.f[2];
+      out->mx[0] = n.f[1]; out->mx[1] = n.f[4] + kEps; out->mx[2] = n.f[3];
+      return true;
+    case RT_NODE_RECT_YZ:
+      out->mn[0] = n.f[4] - kEps; out->mn[1] = n.f[0]; out->mn[2] = n.f[2];
+      out->mx[0] = n.f[4] + kEps; out->mx[1] = n.f[1]; out->mx[2] = n.f[3];
+      return true;
+    case RT_NODE_BVH:
+    case RT_NODE_CUBOID:
+      for (int i = 0; i < 3; ++i) { out->mn[i] = n.f[i]; out->mx[i] = n.f[3 + i]; }
+      return true;
+    case RT_NODE_TRANSLATE: {
+      Box c;
+      if (!flat_box(nodes, n.a, &c)) return false;
+      for (int i = 0; i < 3; ++i) { out->mn[i] = c.mn[i] + n.f[i]; out->mx[i] = c.mx[i] + n.f[i]; }
+      return true;
+    }
+    case RT_NODE_ROTATE: {
+      Box hb;
+      if (!flat_box(nodes, n.a, &hb)) return false;
+      const double s = n.f[0], c = n.f[1];
+      double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+      for (int idx = 26; idx >= 0; --idx) {
+        const double i = idx / 9, j = (idx / 3) % 3, k = idx % 3;
+        const double p0 = i * hb.mx[0] + (1 - i) * hb.mn[0], p1 = j * hb.mx[1] + (1 - j) * hb.mn[1],
+                     p2 = k * hb.mx[2] + (1 - k) * hb.mn[2];
+        double q[3];
+        if (n.b == 0) { q[0] = p0; q[1] = c * p1 - s * p2; q[2] = s * p1 + c * p2; }
+        else if (n.b == 1) { q[0] = c * p0 + s * p2; q[1] = p1; q[2] = -s * p0 + c * p2; }
+        else { q[0] = c * p0 - s * p1; q[1] = s * p0 + c * p1; q[2] = p2; }
+        for (int a = 0; a < 3; ++a) { mn[a] = gmin(q[a], mn[a]); mx[a] = gmax(q[a], mx[a]); }
+      }
+      for (int a = 0; a < 3; ++a) { out->mn[a] = mn[a]; out->mx[a] = mx[a]; }
+      return true;
+    }
+    case RT_NODE_CONSTANT_MEDIUM:
+      return flat_box(nodes, n.a, out);
+    default:
+      return false;
+  }
+}
+
+// Rebuild the world tree rooted at `root` over its leaves; appends nodes, returns the new root
+// (or `root` unchanged when the tree is not eligible). Eligible: no ConstantMedium anywhere
+// under the root, every leaf boundable, finite boxes.
+int rebuild_world_bvh(std::vector<rt_node>& nodes, int root) {
+  std::vector<int> leaves;
+  std::vector<char> seen(nodes.size(), 0);
+  bool ok = true;
+  std::function<void(int)> walk = [&](int id) {
+    if (!ok) return;
+    const rt_node& n = nodes[id];
+    if (n.type == RT_NODE_BVH) {
+      walk(n.a);
+      walk(n.b);
+      return;
+    }
+    std::function<bool(int)> has_media = [&](int k) -> bool {
+      const rt_node& m = nodes[k];
+      if (m.type == RT_NODE_CONSTANT_MEDIUM) return true;
+      if (m.type == RT_NODE_BVH) return has_media(m.a) || has_media(m.b);
+      if (m.type == RT_NODE_TRANSLATE || m.type == RT_NODE_ROTATE) return has_media(m.a);
+      return false;
+    };
+    if (has_media(id) || n.type == RT_NODE_UNHITTABLE || n.type == RT_NODE_EXT) {
+      ok = false;
+      return;
+    }
+    if (!seen[id]) {  // BVHNode h h (src/Lib.hs:948): test the leaf once — a repeat cannot change the hit
+      seen[id] = 1;
+      leaves.push_back(id);
+    }
+  };
+  if (nodes[root].type != RT_NODE_BVH) return root;
+  walk(root);
+  if (!ok || leaves.size() < 2) return root;
+  Builder b{nodes, {}, {}, {}};
+  const int n = (int)leaves.size();
+  b.boxes.resize(n);
+  b.leaf_ids = leaves;
+  for (int a = 0; a < 3; ++a) b.cx[a].resize(n);
+  for (int i = 0; i < n; ++i) {
+    if (!flat_box(nodes, leaves[i], &b.boxes[i])) return root;
+    for (int a = 0; a < 3; ++a) {
+      if (!std::isfinite(b.boxes[i].mn[a]) || !std::isfinite(b.boxes[i].mx[a])) return root;
+      b.cx[a][i] = 0.5 * (b.boxes[i].mn[a] + b.boxes[i].mx[a]);
+    }
+  }
+  std::vector<int> items(n);
+  for (int i = 0; i < n; ++i) items[i] = i;
+  Box rb;
+  return b.build(items, 0, n, rb);
+}
+
+}  // namespace rt
+
+extern "C" int rt_rebuild_bvh(const rt_scene_desc* in, rt_node* out_nodes, int capacity, int* out_n, int* out_root) {
+  if (!in || !out_n || !out_root || !in->nodes || in->n_nodes <= 0 || in->world_root < 0 ||
+      in->world_root >= in->n_nodes) {
+    rt::set_error("rt_rebuild_bvh: bad argument");
+    return RT_E_INVALID;
+  }
+  std::vector<rt_node> nodes(in->nodes, in->nodes + in->n_nodes);
+  const int root = rt::rebuild_world_bvh(nodes, in->world_root);
+  *out_n = (int)nodes.size();
+  *out_root = root;
+  if (out_nodes) {
+    if (capacity < (int)nodes.size()) {
+      rt::set_error("rt_rebuild_bvh: capacity too small");
+      return RT_E_INVALID;
+    }
+    std::copy(nodes.begin(), nodes.end(), out_nodes);
+  }
+  return RT_OK;
+}

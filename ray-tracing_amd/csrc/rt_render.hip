@@ -28,6 +28,10 @@
 #include "rt_internal.h"
 #include "rt_trace.h"
 
+namespace rt {
+int rebuild_world_bvh(std::vector<rt_node>& nodes, int root);
+}
+
 using namespace rtd;
 
 namespace {
@@ -396,6 +400,7 @@ struct rt_ctx {
   unsigned features = 0;
   int n_nodes = 0;
   int stack_need = 0;  // deepest traversal stack the world tree needs (entries)
+  bool rebuilt_bvh = false;
   bool has_scene = false;
   unsigned long long* d_counter = nullptr;
   double last_ms = 0.0;
@@ -748,9 +753,32 @@ void rt_destroy(rt_ctx* c) {
   delete c;
 }
 
-int rt_upload_scene(rt_ctx* c, const rt_scene_desc* d) {
-  if (!c || !d) return invalid("null argument");
+int rt_upload_scene(rt_ctx* c, const rt_scene_desc* d) { return rt_upload_scene_ex(c, d, 0u); }
+
+int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
+  if (!c || !din) return invalid("null argument");
+  if (din->n_nodes <= 0 || !din->nodes || din->world_root < 0 || din->world_root >= din->n_nodes)
+    return invalid("rt_upload_scene: bad node array or world root");
   HIPCHK(hipSetDevice(c->device));
+  // World-tree rebuild (rt_bvh.cpp) unless the caller or RTAMD_REFERENCE_BVH=1 asks for the
+  // reference's own makeBVH tree; never for trees holding media.
+  std::vector<rt_node> nodes(din->nodes, din->nodes + din->n_nodes);
+  rt_scene_desc dd = *din;
+  const char* env = std::getenv("RTAMD_REFERENCE_BVH");
+  const bool keep = (flags & RT_UPLOAD_REFERENCE_BVH) || (env && env[0] == '1');
+  if (!keep) {
+    // validate the original first so the rebuild only ever sees well-formed DAGs
+    Validator v0{din};
+    if (!v0.run()) {
+      rt::set_error("rt_upload_scene: " + v0.err);
+      return v0.code;
+    }
+    dd.world_root = rt::rebuild_world_bvh(nodes, din->world_root);
+  }
+  dd.nodes = nodes.data();
+  dd.n_nodes = (int)nodes.size();
+  const rt_scene_desc* d = &dd;
+  c->rebuilt_bvh = dd.world_root != din->world_root;
   Validator v{d};
   if (!v.run()) {
     rt::set_error("rt_upload_scene: " + v.err);

@@ -31,6 +31,7 @@ RT_NODE_CONSTANT_MEDIUM, RT_NODE_UNHITTABLE, RT_NODE_EXT = 9, 10, 11
 RT_RNG_EXACT, RT_RNG_PHILOX = 0, 1
 RT_FLAG_NAN_CULL = 1
 RT_FLAG_REFERENCE_CULL = 2
+RT_UPLOAD_REFERENCE_BVH = 1
 MATH_OPS = {"div": 0, "div_exact": 1, "sqrt": 2, "sin": 3, "cos": 4, "atan": 5, "asin": 6, "log": 7, "pow": 8,
             "ghc_atan2": 9, "tan": 10}
 
@@ -102,7 +103,7 @@ EXPORTED = [
     "rt_builder_finish", "rt_scene_named", "rt_camera_new", "rt_camera_named", "rt_write_ppm",
     "rt_device_count", "rt_create", "rt_destroy", "rt_upload_scene", "rt_render", "rt_shard_geometry",
     "rt_render_shard_async", "rt_assemble_async", "rt_assemble_linear_async", "rt_last_kernel_ms",
-    "rt_debug_closest_hits", "rt_debug_math", "rt_render_work",
+    "rt_debug_closest_hits", "rt_debug_math", "rt_render_work", "rt_upload_scene_ex", "rt_rebuild_bvh",
 ]
 
 _lib = None
@@ -156,6 +157,8 @@ def lib() -> C.CDLL:
             "rt_debug_closest_hits": (I, [C.c_void_p, P(D), I, D, D, U64, C.c_uint32, P(D)]),
             "rt_debug_math": (I, [C.c_void_p, I, P(D), P(D), I, P(D)]),
             "rt_render_work": (I, [C.c_void_p, P(rt_camera), P(rt_render_params), P(U64)]),
+            "rt_upload_scene_ex": (I, [C.c_void_p, P(rt_scene_desc), C.c_uint32]),
+            "rt_rebuild_bvh": (I, [P(rt_scene_desc), P(rt_node), I, P(I), P(I)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -314,6 +317,23 @@ class Builder:
         return Scene(self, d)
 
 
+def rebuilt_scene(scene: Scene) -> Scene:
+    """The scene as the device traverses it by default: the world tree re-bounded by the SAH
+    rebuild of rt_rebuild_bvh (same leaves, same lights tree)."""
+    n, root = C.c_int(0), C.c_int(0)
+    _check(lib().rt_rebuild_bvh(C.byref(scene.desc), None, 0, C.byref(n), C.byref(root)), "rt_rebuild_bvh")
+    arr = (rt_node * n.value)()
+    _check(lib().rt_rebuild_bvh(C.byref(scene.desc), arr, n.value, C.byref(n), C.byref(root)), "rt_rebuild_bvh")
+    d = rt_scene_desc()
+    C.pointer(d)[0] = scene.desc
+    d.nodes = C.cast(arr, C.POINTER(rt_node))
+    d.n_nodes = n.value
+    d.world_root = root.value
+    s = Scene(scene._builder, d)
+    s._keep = (arr, scene)
+    return s
+
+
 def make_scene(name: str, gen: Tuple[int, int], t0: float = 0.0, t1: float = 1.0,
                earth: Optional[np.ndarray] = None, param: int = 0) -> Tuple[Scene, Tuple[int, int]]:
     """A src/Scenes.hs builder: returns (scene, g1) like `makeXScene t0 t1 gen`."""
@@ -396,8 +416,9 @@ class Context:
         except Exception:
             pass
 
-    def upload(self, scene: Scene):
-        _check(lib().rt_upload_scene(self._h, C.byref(scene.desc)), "rt_upload_scene")
+    def upload(self, scene: Scene, reference_bvh: bool = False):
+        _check(lib().rt_upload_scene_ex(self._h, C.byref(scene.desc), RT_UPLOAD_REFERENCE_BVH if reference_bvh else 0),
+               "rt_upload_scene")
         self._scene = scene
 
     def render(self, cam: rt_camera, params: rt_render_params, col_gens: Optional[np.ndarray] = None,

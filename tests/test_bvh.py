@@ -1,0 +1,69 @@
+"""World-BVH rebuild (CPU): the SAH tree the device traverses by default must give the same
+closest hits as the reference's makeBVH tree (the oracle traverses both with the reference's own
+hit/boxRayIntersect), and must be refused for trees that hold media."""
+import numpy as np
+import pytest
+
+import pyoracle
+import rtamd
+
+
+def _rays(rng, n, center, spread, target):
+    o = np.array(center) + rng.normal(0, spread, (n, 3))
+    d = np.array(target) - o + rng.normal(0, 2.0, (n, 3))
+    return np.concatenate([o, d, rng.uniform(0, 1, (n, 1))], axis=1)
+
+
+@pytest.mark.parametrize("name,center,spread,target", [
+    ("random_book_one", (13.0, 2.0, 3.0), 3.0, (0.0, 0.0, 0.0)),
+    ("three_spheres", (13.0, 2.0, 3.0), 3.0, (0.0, 0.0, 0.0)),
+    ("cornell", (278.0, 278.0, -200.0), 150.0, (278.0, 278.0, 400.0)),
+    ("two_perlin_spheres", (26.0, 4.0, 6.0), 4.0, (0.0, 2.0, 0.0)),
+])
+def test_rebuilt_tree_gives_identical_closest_hits(name, center, spread, target):
+    scene, _ = rtamd.make_scene(name, rtamd.randGen(1024))
+    rebuilt = rtamd.rebuilt_scene(scene)
+    assert rebuilt.desc.world_root != scene.desc.world_root
+    rays = _rays(np.random.default_rng(7), 20000, center, spread, target)
+    a = pyoracle.closest_hits(scene, rays, 1e-4, np.inf)
+    b = pyoracle.closest_hits(rebuilt, rays, 1e-4, np.inf)
+    assert a[:, 0].sum() > 1000
+    assert np.array_equal(a, b)
+
+
+def test_rebuilt_tree_is_a_proper_bvh():
+    scene, _ = rtamd.make_scene("random_book_one", rtamd.randGen(1024))
+    rb = rtamd.rebuilt_scene(scene)
+    nodes = rb.nodes
+    n0 = scene.desc.n_nodes
+    root = rb.desc.world_root
+
+    def leaves(i):
+        nd = nodes[i]
+        if nd["type"] != rtamd.RT_NODE_BVH:
+            return [i]
+        assert nd["a"] < i and nd["b"] < i
+        for ch in (nd["a"], nd["b"]):  # child boxes inside the parent's box
+            if nodes[ch]["type"] == rtamd.RT_NODE_BVH:
+                assert np.all(nodes[ch]["f"][:3] >= nd["f"][:3]) and np.all(nodes[ch]["f"][3:] <= nd["f"][3:])
+        return leaves(nd["a"]) + leaves(nd["b"])
+
+    got = leaves(root)
+    assert len(got) == len(set(got))  # every leaf exactly once
+    ref = set()
+
+    def ref_leaves(i):
+        nd = nodes[i]
+        if nd["type"] == rtamd.RT_NODE_BVH and i < n0:
+            ref_leaves(nd["a"])
+            ref_leaves(nd["b"])
+        else:
+            ref.add(i)
+    ref_leaves(scene.desc.world_root)
+    assert set(got) == ref
+
+
+@pytest.mark.parametrize("name", ["cornell_smoke", "next_week_final"])
+def test_media_trees_are_not_rebuilt(name):
+    scene, _ = rtamd.make_scene(name, rtamd.randGen(1024))
+    assert rtamd.rebuilt_scene(scene).desc.world_root == scene.desc.world_root
