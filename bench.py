@@ -78,6 +78,7 @@ def main():
                     help="RT_FLAG_REFERENCE_CULL: the reference's per-axis box test only (no joint slab filter)")
     ap.add_argument("--reference-bvh", action="store_true",
                     help="traverse the reference's makeBVH world tree (default: SAH rebuild over the same leaves)")
+    ap.add_argument("--spp", type=int, default=0, help="override spp (sampled runs of the big configs; not the metric)")
     ap.add_argument("--tile", type=int, default=16)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     ap.add_argument("--cpu-spp", type=int, default=4)
@@ -102,7 +103,10 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config])
+    if args.spp:
+        cfg["spp"] = args.spp
+        cfg["desc"] += f" [spp overridden to {args.spp}]"
     earth = None
     if cfg.get("earth"):
         earth = np.load(os.path.join(ROOT, "tests", "golden", "earthmap_rgb8.npz"))["rgb"]

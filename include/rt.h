@@ -69,8 +69,11 @@ enum rt_node_type {
  *   ROTATE         f[0] = sin theta, f[1] = cos theta; a = child; b = axis (0 X, 1 Y, 2 Z)
  *   CONSTANT_MEDIUM f[0] = negative inverse density; a = boundary; b = phase material
  * For every type c = htblSize of the node (Lib.hs:662-671): BVH its size, Translate/Rotate
- * the size of the child, Unhittable 0, everything else 1.
+ * the size of the child, Unhittable 0, everything else 1. (World-only BVH nodes appended by the
+ * device-side rebuild carry 0x40000000 | split axis instead; they never occur in a lights tree.)
  */
+#define RT_BVH_ORDERED 0x40000000 /* rebuilt world BVH node: c = this flag | split axis */
+
 typedef struct rt_node {
     double f[6];
     int32_t type;

@@ -32,7 +32,7 @@ struct Builder {
   std::vector<int> leaf_ids;
   std::vector<double> cx[3];
 
-  int emit_bvh(int l, int r, const Box& b, int size) {
+  int emit_bvh(int l, int r, const Box& b, int axis) {
     rt_node n{};
     for (int i = 0; i < 3; ++i) {
       n.f[i] = b.mn[i];
@@ -41,7 +41,7 @@ struct Builder {
     n.type = RT_NODE_BVH;
     n.a = l;
     n.b = r;
-    n.c = size;
+    n.c = RT_BVH_ORDERED | axis;  // world-only node: `c` carries the split axis, not htblSize
     nodes.push_back(n);
     return (int)nodes.size() - 1;
   }
@@ -76,6 +76,12 @@ struct Builder {
       }
     }
     int mid = lo + n / 2;
+    int split_axis = 0;
+    {
+      double best_ext = -1;
+      for (int a = 0; a < 3; ++a)
+        if (cb.mx[a] - cb.mn[a] > best_ext) { best_ext = cb.mx[a] - cb.mn[a]; split_axis = a; }
+    }
     if (n > 2) {
       constexpr int kBins = 16;
       double best = INFINITY;
@@ -121,6 +127,7 @@ struct Builder {
       }
       if (best_axis >= 0) {
         const int a = best_axis;
+        split_axis = a;
         const double ext = cb.mx[a] - cb.mn[a];
         auto it = std::stable_partition(items.begin() + lo, items.begin() + hi, [&](int i) {
           int k = (int)((cx[a][i] - cb.mn[a]) / ext * kBins);
@@ -135,7 +142,17 @@ struct Builder {
     const int l = build(items, lo, mid, bl);
     const int r = build(items, mid, hi, br);
     out = merge(bl, br);
-    return emit_bvh(l, r, out, n);
+    if (n == 2) {  // two leaves: order them along the axis their centroids differ most
+      double best_d = -1;
+      for (int a = 0; a < 3; ++a) {
+        const double dd = std::fabs(cx[a][items[lo]] - cx[a][items[lo + 1]]);
+        if (dd > best_d) { best_d = dd; split_axis = a; }
+      }
+      if (cx[split_axis][items[lo]] > cx[split_axis][items[lo + 1]]) {
+        return emit_bvh(r, l, out, split_axis);
+      }
+    }
+    return emit_bvh(l, r, out, split_axis);
   }
 };
 
@@ -237,7 +254,9 @@ int rebuild_world_bvh(std::vector<rt_node>& nodes, int root) {
   };
   if (nodes[root].type != RT_NODE_BVH) return root;
   walk(root);
-  if (!ok || leaves.size() < 2) return root;
+  // Small trees (e.g. the 8-object Cornell box) keep the reference tree: nothing to gain, and its
+  // visiting order was measured faster there.
+  if (!ok || leaves.size() < 16) return root;
   Builder b{nodes, {}, {}, {}};
   const int n = (int)leaves.size();
   b.boxes.resize(n);

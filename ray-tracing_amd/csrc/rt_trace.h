@@ -420,8 +420,12 @@ __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr
     if (type == RT_NODE_BVH) {
       if constexpr ((F & F_COUNT) != 0) ++cnt.box;
       if (box_hit(n->f, ray, t_min, closest, joint)) {
-        stk[(sp++) * stride] = n->b;
-        node = n->a;
+        // Rebuilt (media-free) trees: visit the child on the ray's side of the split first;
+        // the closest hit is order-independent there. Reference trees stay left-first.
+        const int c = n->c;
+        const bool flip = (c & RT_BVH_ORDERED) && comp(ray.d, c & 3) < 0;
+        stk[(sp++) * stride] = flip ? n->a : n->b;
+        node = flip ? n->b : n->a;
         continue;
       }
     } else if ((F & F_INST) && (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE)) {
