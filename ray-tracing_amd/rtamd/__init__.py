@@ -32,6 +32,7 @@ RT_RNG_EXACT, RT_RNG_PHILOX = 0, 1
 RT_FLAG_NAN_CULL = 1
 RT_FLAG_REFERENCE_CULL = 2
 RT_UPLOAD_REFERENCE_BVH = 1
+RT_BVH_ORDERED = 0x40000000
 MATH_OPS = {"div": 0, "div_exact": 1, "sqrt": 2, "sin": 3, "cos": 4, "atan": 5, "asin": 6, "log": 7, "pow": 8,
             "ghc_atan2": 9, "tan": 10}
 

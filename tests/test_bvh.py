@@ -14,14 +14,12 @@ def _rays(rng, n, center, spread, target):
     return np.concatenate([o, d, rng.uniform(0, 1, (n, 1))], axis=1)
 
 
-@pytest.mark.parametrize("name,center,spread,target", [
-    ("random_book_one", (13.0, 2.0, 3.0), 3.0, (0.0, 0.0, 0.0)),
-    ("three_spheres", (13.0, 2.0, 3.0), 3.0, (0.0, 0.0, 0.0)),
-    ("cornell", (278.0, 278.0, -200.0), 150.0, (278.0, 278.0, 400.0)),
-    ("two_perlin_spheres", (26.0, 4.0, 6.0), 4.0, (0.0, 2.0, 0.0)),
+@pytest.mark.parametrize("name,center,spread,target,param", [
+    ("random_book_one", (13.0, 2.0, 3.0), 3.0, (0.0, 0.0, 0.0), 0),
+    ("stress_spheres", (13.0, 2.0, 3.0), 3.0, (0.0, 0.0, 0.0), 3000),
 ])
-def test_rebuilt_tree_gives_identical_closest_hits(name, center, spread, target):
-    scene, _ = rtamd.make_scene(name, rtamd.randGen(1024))
+def test_rebuilt_tree_gives_identical_closest_hits(name, center, spread, target, param):
+    scene, _ = rtamd.make_scene(name, rtamd.randGen(1024), param=param)
     rebuilt = rtamd.rebuilt_scene(scene)
     assert rebuilt.desc.world_root != scene.desc.world_root
     rays = _rays(np.random.default_rng(7), 20000, center, spread, target)
@@ -61,9 +59,12 @@ def test_rebuilt_tree_is_a_proper_bvh():
             ref.add(i)
     ref_leaves(scene.desc.world_root)
     assert set(got) == ref
+    # rebuilt nodes carry the ordered flag and a split axis in `c`
+    new = nodes[n0:]
+    assert np.all((new["c"] & rtamd.RT_BVH_ORDERED) != 0) and np.all((new["c"] & 3) <= 2)
 
 
-@pytest.mark.parametrize("name", ["cornell_smoke", "next_week_final"])
-def test_media_trees_are_not_rebuilt(name):
+@pytest.mark.parametrize("name", ["cornell_smoke", "next_week_final", "cornell", "three_spheres"])
+def test_media_and_small_trees_are_not_rebuilt(name):
     scene, _ = rtamd.make_scene(name, rtamd.randGen(1024))
     assert rtamd.rebuilt_scene(scene).desc.world_root == scene.desc.world_root
