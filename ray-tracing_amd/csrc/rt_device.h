@@ -60,7 +60,7 @@ struct Ray {
 // non-finite operands included). Bit-identical to `a / b` (tests/test_gpu_math.py).
 __device__ __forceinline__ bool in_range(double x) {
   const double ax = fabs(x);
-  return ax >= 0x1p-900 && ax <= 0x1p900;
+  return (ax >= 0x1p-900) & (ax <= 0x1p900);
 }
 __device__ __forceinline__ double div_exact(double a, double b, double y) {
   double q = a * y;
@@ -73,7 +73,7 @@ __device__ __forceinline__ double div_exact(double a, double b, double y) {
 }
 
 // A ray plus the per-ray reciprocals the exact divisions use. `safe` = every divisor in
-// [2^-500, 2^500] (else all divisions take the IEEE path).
+// [2^-900, 2^900] and a finite origin (else all divisions take the IEEE path).
 struct RayX {
   V3 o, d;
   double tm;
@@ -91,7 +91,8 @@ __device__ __forceinline__ RayX prep(const Ray& r) {
   x.inv = V3{1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z};
   x.a = r.d.x * r.d.x + r.d.y * r.d.y + r.d.z * r.d.z;
   x.inva = 1.0 / x.a;
-  x.safe = div_ok(r.d.x) && div_ok(r.d.y) && div_ok(r.d.z) && div_ok(x.a);
+  x.safe = div_ok(r.d.x) & div_ok(r.d.y) & div_ok(r.d.z) & div_ok(x.a) &
+           (fabs(r.o.x) <= 0x1p900) & (fabs(r.o.y) <= 0x1p900) & (fabs(r.o.z) <= 0x1p900);
   return x;
 }
 __device__ __forceinline__ Ray plain(const RayX& x) { return Ray{x.o, x.d, x.tm}; }

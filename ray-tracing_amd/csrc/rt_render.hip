@@ -56,6 +56,7 @@ struct RenderArgs {
   uint64_t seed;
   unsigned long long* counter;
   unsigned long long* work;  // counting build: [segments, box, prim, other, light, blocks, samples]
+  int trav_stop;             // replacement loop: keep stepping while > trav_stop/64 of live lanes walk
   uint8_t* out_rgb;  // tier B: slab; tier A: image
   double* out_lin;
   uint64_t* gens;  // tier A: per-column (seed, gamma), updated in place
@@ -139,6 +140,37 @@ __device__ __forceinline__ bool segment(const RenderArgs& A, const Scene& S, Ray
     thr = vmul(thr, s.att);
   } else {
     const double c = dot(h.n, s.ray.d);  // scatteringPdf (Lib.hs:874-878)
+    const double spdf = c < 0 ? 0 : c / kPi;
+    const double k = spdf / s.pdf;
+    thr = vmul(thr, scale(k, s.att));
+  }
+  ray = s.ray;
+  --depth;
+  return false;
+}
+
+// The rest of a segment once its closest hit is known (rayColor, Lib.hs:1309-1333): background,
+// emission, or a scatter. Returns true when the path ends (contribution in `contrib`).
+template <unsigned F, class R>
+__device__ __forceinline__ bool shade_hit(const Scene& S, bool got, const Hit& h, Ray& ray, V3& thr, int& depth, R& g,
+                                          V3& contrib, Cnt& cnt) {
+  if (!got) {
+    contrib = vmul(thr, v3(S.bg[0], S.bg[1], S.bg[2]));
+    return true;
+  }
+  const DMat m = S.mats[h.mat];
+  if (m.type == RT_MAT_DIFFUSE_LIGHT) {
+    const V3 e = h.ff ? v3(0, 0, 0) : texture_value<F>(S, m.tex, h.u, h.v, h.p);
+    contrib = vmul(thr, e);
+    return true;
+  }
+  Scatter s;
+  if constexpr ((F & F_COUNT) != 0) cnt.light += (m.type == RT_MAT_LAMBERTIAN && S.lights >= 0);
+  scatter<F>(S, m, ray, h, g, s);
+  if (s.specular) {
+    thr = vmul(thr, s.att);
+  } else {
+    const double c = dot(h.n, s.ray.d);
     const double spdf = c < 0 ? 0 : c / kPi;
     const double k = spdf / s.pdf;
     thr = vmul(thr, scale(k, s.att));
@@ -279,6 +311,165 @@ __global__ void __launch_bounds__(WAVES * 256, WAVES) render_philox_lds(RenderAr
   philox_loop<F>(A, S, stk, WAVES * 256);
 }
 
+
+// Tier-B loop with ray replacement (media-free worlds without instance frames): traversal state
+// persists in registers across iterations; each iteration first shades the lanes whose walk has
+// ended and starts their next segment (or sample, or pixel), then steps every walking lane one
+// node at a time until at most trav_stop/64 of the live lanes are still walking. Lanes never
+// wait for the slowest walk of their wave, and shading runs for many lanes at once.
+template <unsigned F>
+__device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S, int* stk, int stride) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const bool joint = !(A.flags & RT_FLAG_REFERENCE_CULL);
+
+  long long w = -1;
+  bool done = false, path = false, walking = false, ready = false;
+  int px = 0, row = 0, s = 0, depth = 0;
+  Ray ray;
+  V3 thr = v3(0, 0, 0), sum = v3(0, 0, 0);
+  RngPhilox g;
+  g.init(A.seed, 0, 0);
+  Trav t;
+  Cnt cnt{0, 0, 0, 0};
+  unsigned long long segs = 0, blocks = 0, samples = 0, ph_setup = 0, ph_trav = 0;
+
+  for (;;) {
+    unsigned long long s0 = 0;
+    if constexpr ((F & F_COUNT) != 0) s0 = stamp();
+    // ---- shade finished walks, then set up the next walk for every lane that is not walking
+    if (ready) {
+      ready = false;
+      Hit h;
+      const bool got = trav_finish<F>(S, t, ray, kEps, h);
+      V3 contrib;
+      if (shade_hit<F>(S, got, h, ray, thr, depth, g, contrib, cnt)) {
+        if constexpr ((F & F_COUNT) != 0) {
+          blocks += g.pair;
+          ++samples;
+        }
+        sum = sum + contrib;
+        path = false;
+        ++s;
+        const bool all_nan = (A.flags & RT_FLAG_NAN_CULL) && sum.x != sum.x && sum.y != sum.y && sum.z != sum.z;
+        if (s == A.spp || all_nan) {
+          store_pixel(A, w, divide(sum, (double)A.spp));
+          w = -1;
+        }
+      }
+    }
+    while (!walking) {
+      // acquire pixels for idle lanes: one atomic per round for all of them
+      for (;;) {
+        const bool need = (w < 0) && !done;
+        const unsigned long long mask = __ballot(need);
+        if (!mask) break;
+        const int leader = __ffsll((long long)mask) - 1;
+        unsigned long long base = 0;
+        if (lane == leader) base = atomicAdd(A.counter, (unsigned long long)__popcll(mask));
+        base = __shfl(base, leader);
+        if (need) {
+          const long long wi = (long long)(base + __popcll(mask & lanes_below));
+          if (wi >= A.work_total) {
+            done = true;
+          } else if (work_pixel(A, wi, px, row)) {
+            w = wi;
+            s = 0;
+            sum = v3(0, 0, 0);
+            path = false;
+          }
+        }
+      }
+      if (w < 0) break;  // no work left for this lane
+      if (!path) {  // start sample s: uniformRandomUVs' pair, then getRay
+        const uint32_t pid = (uint32_t)((long long)row * A.W + px);
+        g.init(A.seed, pid, (uint32_t)s);
+        const double ru = g.draw(), rv = g.draw();
+        const int y = A.H - 1 - row;
+        const double u = ((double)px + ru) / (double)A.W;
+        const double v = ((double)y + rv) / (double)A.H;
+        ray = get_ray(A.cam, u, v, g);
+        thr = v3(1.0, 1.0, 1.0);
+        depth = A.max_depth;
+        path = true;
+      }
+      if (depth <= 0) {  // d <= 0 -> black; the sample ends without a walk
+        if constexpr ((F & F_COUNT) != 0) {
+          blocks += g.pair;
+          ++samples;
+        }
+        sum = sum + vmul(thr, v3(0.0, 0.0, 0.0));
+        path = false;
+        ++s;
+        const bool all_nan = (A.flags & RT_FLAG_NAN_CULL) && sum.x != sum.x && sum.y != sum.y && sum.z != sum.z;
+        if (s == A.spp || all_nan) {
+          store_pixel(A, w, divide(sum, (double)A.spp));
+          w = -1;
+        }
+        continue;
+      }
+      trav_begin(t, ray, S.world, INFINITY);
+      walking = true;
+      if constexpr ((F & F_COUNT) != 0) ++segs;
+    }
+    if (!walking) break;  // this lane is finished; the rest of the wave carries on without it
+    unsigned long long s1 = 0;
+    if constexpr ((F & F_COUNT) != 0) s1 = stamp();
+    // ---- walk until few lanes are still walking
+    const int live = __popcll(__ballot(true));
+    const int stop = (live * A.trav_stop) >> 6;
+    for (;;) {
+      if (__popcll(__ballot(walking)) <= stop) break;
+      if (walking) {
+        walking = trav_step<F>(S, t, kEps, stk, stride, joint, cnt);
+        ready = !walking;
+      }
+    }
+    if constexpr ((F & F_COUNT) != 0) {
+      const unsigned long long s2 = stamp();
+      ph_setup += s1 - s0;
+      ph_trav += s2 - s1;
+    }
+  }
+  if constexpr ((F & F_COUNT) != 0) {
+    wave_add(&A.work[0], segs);
+    wave_add(&A.work[1], cnt.box);
+    wave_add(&A.work[2], cnt.prim);
+    wave_add(&A.work[3], cnt.other);
+    wave_add(&A.work[4], cnt.light);
+    wave_add(&A.work[5], blocks);
+    wave_add(&A.work[6], samples);
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(&A.work[8], ph_setup);  // shading + setup (reported as "acquire_camera" + "shade")
+      atomicAdd(&A.work[9], ph_trav);
+    }
+  }
+}
+
+template <unsigned F, int WAVES>
+__global__ void __launch_bounds__(RT_BLOCK, WAVES) render_philox2(RenderArgs A) {
+  __shared__ int stk_mem[RT_STACK * RT_BLOCK];
+  philox_loop2<F>(A, A.S, &stk_mem[threadIdx.x], RT_BLOCK);
+}
+
+template <unsigned F, int WAVES>
+__global__ void __launch_bounds__(WAVES * 256, WAVES) render_philox2_lds(RenderArgs A, int n_nodes, int stack_entries) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  rt_node* nodes = reinterpret_cast<rt_node*>(lds);
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(A.S.nodes);
+    uint4* dst = reinterpret_cast<uint4*>(lds);
+    const int n16 = n_nodes * (int)(sizeof(rt_node) / 16);
+    for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  Scene S = A.S;
+  S.nodes = nodes;
+  int* stk = reinterpret_cast<int*>(lds + (size_t)n_nodes * sizeof(rt_node)) + threadIdx.x;
+  (void)stack_entries;
+  philox_loop2<F>(A, S, stk, WAVES * 256);
+}
+
 // ---------------------------------------------------------------- tier A: the reference's stream
 // One lane per image column; rows top to bottom; each pixel draws its 2*ns UVs first and uses
 // them in reverse draw order (uniformRandomUVs' foldr, Lib.hs:1358-1371) — the UV pairs are
@@ -401,6 +592,7 @@ struct rt_ctx {
   int n_nodes = 0;
   int stack_need = 0;  // deepest traversal stack the world tree needs (entries)
   bool rebuilt_bvh = false;
+  bool replace_ok = false;  // media-free and no instance frames: the replacement loop applies
   bool has_scene = false;
   unsigned long long* d_counter = nullptr;
   double last_ms = 0.0;
@@ -600,29 +792,41 @@ int waves_target(int dflt) {
   const int w = e ? std::atoi(e) : dflt;
   return (w >= 1 && w <= 4) ? w : dflt;
 }
-template <unsigned F>
-const void* by_waves(int w) {
-  if (w == 2) return (const void*)render_philox<F, 2>;
-  if (w == 3) return (const void*)render_philox<F, 3>;
-  if (w == 4) return (const void*)render_philox<F, 4>;
-  return (const void*)render_philox<F, 1>;
-}
-const void* philox_variant(unsigned f, bool count) {
-  switch (variant_for(f)) {
-    case kVarSpheres:
-      return count ? (const void*)render_philox<kVarSpheres | F_COUNT, 1> : by_waves<kVarSpheres>(waves_target(3));
-    case kVarCornell:
-      return count ? (const void*)render_philox<kVarCornell | F_COUNT, 1> : by_waves<kVarCornell>(waves_target(1));
-    default: return count ? (const void*)render_philox<F_ALL | F_COUNT, 1> : (const void*)render_philox<F_ALL, 1>;
+// Kernel pointer for (variant, replacement loop?, LDS-staged?, waves per SIMD, counting build?).
+template <unsigned V>
+const void* pick(bool replace, bool lds, int w, bool count) {
+  if (count) return replace ? (const void*)render_philox2<V | F_COUNT, 1> : (const void*)render_philox<V | F_COUNT, 1>;
+  if (lds) {
+    if (replace) {
+      if (w == 2) return (const void*)render_philox2_lds<V, 2>;
+      if (w == 4) return (const void*)render_philox2_lds<V, 4>;
+      if (w == 1) return (const void*)render_philox2_lds<V, 1>;
+      return (const void*)render_philox2_lds<V, 3>;
+    }
+    if (w == 2) return (const void*)render_philox_lds<V, 2>;
+    if (w == 4) return (const void*)render_philox_lds<V, 4>;
+    if (w == 1) return (const void*)render_philox_lds<V, 1>;
+    return (const void*)render_philox_lds<V, 3>;
   }
-}
-const void* lds_variant(unsigned var, int waves) {
-  if (var == kVarSpheres) {
-    if (waves == 2) return (const void*)render_philox_lds<kVarSpheres, 2>;
-    if (waves == 4) return (const void*)render_philox_lds<kVarSpheres, 4>;
-    return (const void*)render_philox_lds<kVarSpheres, 3>;
+  if (replace) {
+    if (w == 2) return (const void*)render_philox2<V, 2>;
+    if (w == 3) return (const void*)render_philox2<V, 3>;
+    if (w == 4) return (const void*)render_philox2<V, 4>;
+    return (const void*)render_philox2<V, 1>;
   }
-  return (const void*)render_philox_lds<kVarCornell, 1>;
+  if (w == 2) return (const void*)render_philox<V, 2>;
+  if (w == 3) return (const void*)render_philox<V, 3>;
+  if (w == 4) return (const void*)render_philox<V, 4>;
+  return (const void*)render_philox<V, 1>;
+}
+const void* philox_kernel(unsigned var, bool replace, bool lds, int w, bool count) {
+  if (var == kVarSpheres) return pick<kVarSpheres>(replace, lds, w, count);
+  if (var == kVarCornell) return pick<kVarCornell>(replace, lds, w, count);
+  return count ? (const void*)render_philox<F_ALL | F_COUNT, 1> : (const void*)render_philox<F_ALL, 1>;
+}
+bool env_off(const char* name) {
+  const char* e = std::getenv(name);
+  return e && e[0] == '0';
 }
 const void* exact_variant(unsigned f) {
   switch (variant_for(f)) {
@@ -675,18 +879,21 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   A.out_rgb = d_rgb;
   A.out_lin = d_lin;
   HIPCHK(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned long long), st));
+  const char* stop_env = std::getenv("RTAMD_TRAV_STOP");
+  A.trav_stop = stop_env ? std::max(0, std::min(63, std::atoi(stop_env))) : 16;
+  const unsigned var = variant_for(c->features);
+  const bool count = d_work != nullptr;
+  // Replacement loop for media-free worlds without instance frames (RTAMD_REPLACE=0 disables).
+  const bool replace = c->replace_ok && var != F_ALL && !env_off("RTAMD_REPLACE");
+  const int waves = var == kVarSpheres ? waves_target(3) : waves_target(1);
   // LDS-staged kernel when the node array plus the traversal stack fit one CU's 160 KiB
   // (RTAMD_LDS=0 disables it for A/B runs).
-  const char* lds_env = std::getenv("RTAMD_LDS");
-  const bool lds_ok = !(lds_env && lds_env[0] == '0') && d_work == nullptr;
-  const unsigned var = variant_for(c->features);
-  if (lds_ok && (var == kVarSpheres || var == kVarCornell)) {
-    const int waves = var == kVarSpheres ? waves_target(3) : 1;
+  if (!count && !env_off("RTAMD_LDS") && var != F_ALL) {
     const int block = waves * 256;
     const int entries = c->stack_need + 2;
     const size_t bytes = (size_t)c->n_nodes * sizeof(rt_node) + (size_t)entries * block * sizeof(int);
     if (bytes <= 160 * 1024) {
-      const void* fn = lds_variant(var, waves);
+      const void* fn = philox_kernel(var, replace, true, waves, false);
       HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
       int n_nodes = c->n_nodes;
       void* args[] = {&A, &n_nodes, (void*)&entries};
@@ -696,7 +903,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
       return RT_OK;
     }
   }
-  const void* fn = philox_variant(c->features, d_work != nullptr);
+  const void* fn = philox_kernel(var, replace, false, count ? 1 : waves, count);
   int bpc = 1;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, RT_BLOCK, 0));
   const long long want = (slab + RT_BLOCK - 1) / RT_BLOCK;
@@ -732,7 +939,7 @@ int rt_create(int device, rt_ctx** out) {
   HIPCHK(hipGetDeviceProperties(&prop, device));
   c->cu_count = prop.multiProcessorCount;
   int bpc = 0;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, render_philox<F_ALL, 1>, RT_BLOCK, 0));
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void*)render_philox<F_ALL, 1>, RT_BLOCK, 0));
   c->blocks_per_cu = bpc;
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIPCHK(hipEventCreate(&c->ev0));
@@ -829,6 +1036,11 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
   c->features = scene_features(d);
   c->n_nodes = d->n_nodes;
   c->stack_need = v.stack_need[d->world_root];
+  c->replace_ok = !(c->features & F_MEDIA);
+  for (const rt_node& x : v.nodes)
+    if (((x.type & RT_TYPE_MASK) == RT_NODE_TRANSLATE || (x.type & RT_TYPE_MASK) == RT_NODE_ROTATE) &&
+        !(x.type & RT_CHAIN_PRIM))
+      c->replace_ok = false;
   c->has_scene = true;
   return RT_OK;
 }

@@ -94,7 +94,7 @@ __device__ __forceinline__ double div_mk(double a, double b, double y) {
   return fma(r, y, q);
 }
 // quotient and dividend both in the trusted range (divisors are covered by RayX::safe)
-__device__ __forceinline__ bool q_ok(double a, double q) { return in_range(a) && in_range(q); }
+__device__ __forceinline__ bool q_ok(double a, double q) { return in_range(a) & in_range(q); }
 
 // boxRayIntersect (Lib.hs:798-814): per axis, [max t0 t_min, min t1 t_max] must be non-empty,
 // with the reference's quotients (bit-exact) and GHC max/min. The reference never intersects the
@@ -102,31 +102,14 @@ __device__ __forceinline__ bool q_ok(double a, double q) { return in_range(a) &&
 // lower bounds < min of the upper bounds). That accepts a subset of the reference's boxes, so it
 // only prunes subtrees; what it prunes cannot hold a hit in [t_min, t_max] except exactly on a box
 // face (measure zero; tests/test_gpu_parity.py checks closest hits bit for bit).
-__device__ __forceinline__ bool box_hit_exact(const double* f, const RayX& r, double t_min, double t_max,
-                                              bool joint) {
-  double q[6];
-  bool good = r.safe;
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    const double o = comp(r.o, a), d = comp(r.d, a), y = comp(r.inv, a);
-    const double n0 = f[a] - o, n1 = f[a + 3] - o;
-    q[2 * a] = div_mk(n0, d, y);
-    q[2 * a + 1] = div_mk(n1, d, y);
-    good = good && q_ok(n0, q[2 * a]) && q_ok(n1, q[2 * a + 1]);
-  }
-  if (!good) {
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      const double o = comp(r.o, a), d = comp(r.d, a);
-      q[2 * a] = (f[a] - o) / d;
-      q[2 * a + 1] = (f[a + 3] - o) / d;
-    }
-  }
+__device__ __forceinline__ bool box_hit_exact(const double* f, const RayX& r, double t_min, double t_max, bool joint) {
   bool ok = true;
   double lmax = t_min, hmin = t_max;
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
-    const double ta = q[2 * a], tb = q[2 * a + 1];
+    const double o = comp(r.o, a), d = comp(r.d, a);
+    const double ta = (f[a] - o) / d;
+    const double tb = (f[a + 3] - o) / d;
     const bool lt = ta < tb;
     const double t0 = lt ? ta : tb, t1 = lt ? tb : ta;
     const double lo = gmax(t0, t_min);
@@ -141,26 +124,27 @@ __device__ __forceinline__ bool box_hit_exact(const double* f, const RayX& r, do
 // The default (joint) test decided without divisions. When every quotient is finite and
 // non-NaN, (reference per-axis test) AND (joint test) is exactly L < U with
 // L = max(t_min, min(ta,tb) over axes) and U = min(t_max, max(ta,tb) over axes), and L and U are
-// each one of the exact quotients (or t_min / t_max). q' = n * RN(1/d) is within 2^-51 |q| of the
-// exact quotient q = RN(n / d), so L' and U' (same max/min over q') are within 2^-50 of L and U;
-// outside the band |U' - L'| <= 2^-48 (|L'| + |U'|) the sign of U' - L' is the sign of U - L.
-// Inside the band, or when any operand leaves the trusted range, the exact test decides.
+// each one of the exact quotients (or t_min / t_max). For a `safe` ray (finite origin, every
+// |d| in [2^-900, 2^900] so y = RN(1/d) is normal) q' = n * y is within 2^-51 |q| + 2^-1074 of
+// q = RN(n / d), so L', U' are within 2^-50 (|L'| + |U'|) + 2^-1073 of L, U: outside the band
+// U' - L' in [-b, b], b = 2^-48 (|L'| + |U'|) (> 2^-1000 whenever the decision is taken), the
+// sign of U' - L' is the sign of U - L. Overflowed, NaN or banded cases fall through to the
+// exact test. Branch-free except for that (rare) fall-through.
 __device__ __forceinline__ bool box_hit(const double* f, const RayX& r, double t_min, double t_max, bool joint) {
   if (!joint) return box_hit_exact(f, r, t_min, t_max, false);
   double L = t_min, U = t_max;
-  bool good = r.safe;
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     const double o = comp(r.o, a), y = comp(r.inv, a);
-    const double n0 = f[a] - o, n1 = f[a + 3] - o;
-    const double ta = n0 * y, tb = n1 * y;
-    good = good && in_range(n0) && in_range(n1) && fabs(ta) <= 0x1p900 && fabs(tb) <= 0x1p900;
+    const double ta = (f[a] - o) * y, tb = (f[a + 3] - o) * y;
     L = fmax(L, fmin(ta, tb));
     U = fmin(U, fmax(ta, tb));
   }
   const double band = 0x1p-48 * (fabs(L) + fabs(U));
-  if (good && U - L > band) return true;
-  if (good && L - U > band) return false;
+  const bool ok_band = band > 0x1p-1000;
+  const bool yes = r.safe & ok_band & (U - L > band);
+  const bool no = r.safe & ok_band & (L - U > band);
+  if (yes | no) return yes;
   return box_hit_exact(f, r, t_min, t_max, true);
 }
 
@@ -212,7 +196,7 @@ __device__ __forceinline__ bool sphere_t(V3 sc, double sr, const RayX& r, double
   const double sd = sqrt(disc);
   const double n1 = (-b) - sd, n2 = (-b) + sd;
   double temp1 = div_mk(n1, a, r.inva), temp2 = div_mk(n2, a, r.inva);
-  if (!(r.safe && q_ok(n1, temp1) && q_ok(n2, temp2))) {
+  if (!(r.safe & q_ok(n1, temp1) & q_ok(n2, temp2))) {
     temp1 = n1 / a;
     temp2 = n2 / a;
   }
@@ -498,6 +482,77 @@ __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr
       ray = prep(pr);
     }
   }
+}
+
+// ------------------------------------------------------------------ resumable traversal
+// The same depth-first closest-hit walk as `traverse`, one node per call, with its state kept in
+// registers between calls (stack in LDS), for worlds without ConstantMedium and without instance
+// frames (instances over primitive chains are leaves here). Lets a wave keep every lane busy:
+// lanes whose walk has ended are shaded and restarted while the others keep walking.
+struct Trav {
+  RayX ray;
+  double closest;    // current bound (closest hit so far)
+  double best_tmax;  // chain hits: the bound in force when the best hit was found
+  int node, sp, best_node, best_sub;
+};
+
+__device__ __forceinline__ void trav_begin(Trav& t, const Ray& r, int root, double t_max) {
+  t.ray = prep(r);
+  t.closest = t_max;
+  t.best_tmax = t_max;
+  t.node = root;
+  t.sp = 0;
+  t.best_node = -1;
+  t.best_sub = 0;
+}
+
+// Visit one node; false once the walk is over.
+template <unsigned F>
+__device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min, int* stk, int stride, bool joint,
+                                          Cnt& cnt) {
+  const rt_node* n = &S.nodes[t.node];
+  const int type = n->type & RT_TYPE_MASK;
+  if (type == RT_NODE_BVH) {
+    if constexpr ((F & F_COUNT) != 0) ++cnt.box;
+    if (box_hit(n->f, t.ray, t_min, t.closest, joint)) {
+      const int c = n->c;
+      const bool flip = (c & RT_BVH_ORDERED) && comp(t.ray.d, c & 3) < 0;
+      stk[(t.sp++) * stride] = flip ? n->a : n->b;
+      t.node = flip ? n->b : n->a;
+      return true;
+    }
+  } else if ((F & F_INST) && (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE)) {
+    if constexpr ((F & F_COUNT) != 0) ++cnt.other;
+    Hit h;
+    if (chain_hit<F>(S, t.node, plain(t.ray), t_min, t.closest, h)) {
+      t.best_tmax = t.closest;
+      t.closest = h.t;
+      t.best_node = t.node;
+      t.best_sub = -1;
+    }
+  } else {
+    if constexpr ((F & F_COUNT) != 0) ++cnt.prim;
+    double tt;
+    int sub;
+    if (prim_t<F>(S, n, t.ray, t_min, t.closest, tt, sub)) {
+      t.closest = tt;
+      t.best_node = t.node;
+      t.best_sub = sub;
+    }
+  }
+  if (t.sp == 0) return false;
+  t.node = stk[(--t.sp) * stride];
+  return true;
+}
+
+// The closest hit's record, built once from the same ray with the same operations (a chain
+// hit is re-run under the bound that was in force when it was found).
+template <unsigned F>
+__device__ __forceinline__ bool trav_finish(const Scene& S, const Trav& t, const Ray& r, double t_min, Hit& h) {
+  if (t.best_node < 0) return false;
+  if (t.best_sub < 0) return chain_hit<F>(S, t.best_node, r, t_min, t.best_tmax, h);
+  prim_record<F>(S, &S.nodes[t.best_node], t.best_sub, r, t.closest, h);
+  return true;
 }
 
 // ------------------------------------------------------------------ lights (Lib.hs:662-724)
