@@ -67,6 +67,36 @@ def cpu_baseline(cfg, scene, cam, threads, spp_sample):
     return samples / dt / 1e6, dt, cnt
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def pmc_traffic(args, kernel_ms):
+    """HBM traffic of the render kernel from the committed rocprofv3 PMC summary of the same
+    config (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE, bytes per launch), as GB/s over
+    this run's live kernel time. None when no summary matches the launched kernel selection."""
+    path = args.traffic_json or os.path.join(ROOT, "profiles", f"r1_pmc_{args.config}.json")
+    default_sel = not any(k.startswith("RTAMD_") for k in os.environ) and not (
+        args.nan_cull or args.reference_cull or args.reference_bvh or args.spp or args.tile != 16)
+    if not os.path.exists(path) or not (default_sel or args.traffic_json):
+        return None, "no PMC summary for this kernel selection"
+    with open(path) as f:
+        s = json.load(f)
+    b = s.get("derived", {}).get("hbm_bytes")
+    if b is None:
+        return None, f"{os.path.basename(path)} has no FETCH_SIZE/WRITE_SIZE"
+    return round(b / (kernel_ms * 1e-3) / 1e9, 3), (
+        f"{os.path.relpath(path, ROOT)}: {b / 1e6:.1f} MB/launch HBM (FETCH_SIZE x2 + WRITE_SIZE) over the "
+        f"live kernel time; profiled launch {s['avg_duration_s'] * 1e3:.1f} ms")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -81,9 +111,13 @@ def main():
     ap.add_argument("--spp", type=int, default=0, help="override spp (sampled runs of the big configs; not the metric)")
     ap.add_argument("--tile", type=int, default=16)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-    ap.add_argument("--cpu-spp", type=int, default=4)
+    ap.add_argument("--cpu-spp", type=int, default=0,
+                    help="spp of the bounded CPU sample (default: ~40 M samples, ~10 s on 16 cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-work", action="store_true", help="skip the counting-build pass")
+    ap.add_argument("--traffic-json", default="",
+                    help="PMC summary (scripts/pmc_summary.py) of this config's render kernel; default "
+                         "profiles/r1_pmc_<config>.json when the run uses the default kernel selection")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI, default) or gloo (rehearsal: host-staged gather)")
     args = ap.parse_args()
@@ -201,8 +235,11 @@ def main():
         cb = None
         counters = None
         if not args.no_cpu_baseline:
+            if not args.cpu_spp:
+                args.cpu_spp = max(1, min(cfg["spp"], round(40e6 / (cfg["W"] * cfg["H"]))))
             v, dt, counters = cpu_baseline(cfg, scene, cam, args.cpu_threads, args.cpu_spp)
             cb = {"value": round(v, 4), "unit": "Msamples/s", "cores": args.cpu_threads, "kind": "port",
+                  "cpu": cpu_model(),
                   "sample": f"full {cfg['W']}x{cfg['H']} frame at {args.cpu_spp} spp (tier-B streams 0..{args.cpu_spp - 1}"
                             f" of every pixel), {dt:.1f} s, oracle/oracle.c fp64 glibc -O2 OpenMP"}
         out["cpu_baseline"] = cb
@@ -215,8 +252,10 @@ def main():
             samples_per_launch = samples_frame / world
             achieved = bytes_per_sample * samples_per_launch / (kernel_avg * 1e-3) / 1e9
             fl = flops_per_sample * samples_per_launch / (kernel_avg * 1e-3) / 1e12
+            traffic, tnote = pmc_traffic(args, kernel_avg)
             out["roofline"] = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                               "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                               "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                               "traffic_note": tnote,
                                "kernel_ms": round(kernel_avg, 3),
                                "bytes_per_sample": round(bytes_per_sample, 2),
                                "note": "algorithmic scene-record bytes per sample, device-counted by the counting "

@@ -332,7 +332,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
   g.init(A.seed, 0, 0);
   Trav t;
   Cnt cnt{0, 0, 0, 0};
-  unsigned long long segs = 0, blocks = 0, samples = 0, ph_setup = 0, ph_trav = 0;
+  unsigned long long segs = 0, blocks = 0, samples = 0, ph_setup = 0, ph_trav = 0, ph_shade = 0;
 
   for (;;) {
     unsigned long long s0 = 0;
@@ -358,6 +358,8 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
         }
       }
     }
+    unsigned long long s0b = 0;
+    if constexpr ((F & F_COUNT) != 0) s0b = stamp();
     while (!walking) {
       // acquire pixels for idle lanes: one atomic per round for all of them
       for (;;) {
@@ -427,7 +429,8 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     }
     if constexpr ((F & F_COUNT) != 0) {
       const unsigned long long s2 = stamp();
-      ph_setup += s1 - s0;
+      ph_shade += s0b - s0;
+      ph_setup += s1 - s0b;
       ph_trav += s2 - s1;
     }
   }
@@ -440,8 +443,9 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     wave_add(&A.work[5], blocks);
     wave_add(&A.work[6], samples);
     if ((threadIdx.x & 63) == 0) {
-      atomicAdd(&A.work[8], ph_setup);  // shading + setup (reported as "acquire_camera" + "shade")
+      atomicAdd(&A.work[8], ph_setup);
       atomicAdd(&A.work[9], ph_trav);
+      atomicAdd(&A.work[10], ph_shade);
     }
   }
 }
