@@ -334,9 +334,9 @@ int rt_assemble_linear_async(rt_ctx* ctx, const rt_render_params* p, const doubl
 
 /*
  * Counting build of the tier-B render (same output, slower): device-measured work for the
- * roofline. out_work[0..6] = {segments traced, BVH box tests, leaf primitive tests,
- * instance/medium tests, light-pdf evaluations, Philox blocks, samples} for this shard;
- * out_work[8..10] = wave time (s_memtime ticks, summed over waves) spent acquiring work and
+ * roofline. out_work[0..7] = {segments traced, BVH box tests, leaf primitive tests,
+ * instance/medium tests, light-pdf evaluations, Philox blocks, samples, 4-wide node visits}
+ * for this shard; out_work[8..10] = wave time (s_memtime ticks, summed over waves) spent acquiring work and
  * starting samples / traversing / shading; the rest 0.
  */
 int rt_render_work(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* p, uint64_t out_work[16]);
@@ -348,7 +348,13 @@ int rt_last_kernel_ms(rt_ctx* ctx, double* out_ms);
  * Debug / parity entry: closest hit of n world rays (7 doubles each: origin, direction, time)
  * in [tmin, tmax]. out: 12 doubles per ray: hit(0/1), t, p xyz, normal xyz, u, v, front_face,
  * material. Media draws use tier-B stream (seed, pixel_id = ray index, sample 0).
+ * flags: RT_FLAG_REFERENCE_CULL as for rendering, plus one walk selector: none = the recursive
+ * walk (media and frames allowed); RT_DEBUG_RESUMABLE = the render loop's resumable binary
+ * walk; RT_DEBUG_WIDE = the resumable walk over the 4-wide fp32-box tree. The last two need a
+ * world without ConstantMedium and instance frames (else RT_E_UNSUPPORTED).
  */
+#define RT_DEBUG_RESUMABLE 4u
+#define RT_DEBUG_WIDE 8u
 int rt_debug_closest_hits(rt_ctx* ctx, const double* rays, int n, double tmin, double tmax,
                           uint64_t seed, uint32_t flags, double* out);
 

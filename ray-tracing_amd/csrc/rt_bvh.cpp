@@ -17,6 +17,7 @@
 
 #include "rt.h"
 #include "rt_internal.h"
+#include "rt_wide.h"
 
 namespace rt {
 
@@ -273,6 +274,99 @@ int rebuild_world_bvh(std::vector<rt_node>& nodes, int root) {
   for (int i = 0; i < n; ++i) items[i] = i;
   Box rb;
   return b.build(items, 0, n, rb);
+}
+
+namespace {
+
+// Nearest float below / above a double (the fp32 box contains the fp64 one).
+float f32_down(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = std::nextafter(f, -INFINITY);
+  return f;
+}
+float f32_up(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = std::nextafter(f, INFINITY);
+  return f;
+}
+
+struct WideBuilder {
+  const std::vector<rt_node>& nodes;
+  std::vector<rt_wnode>& out;
+  bool ok = true;
+
+  bool box_of(int id, Box& b) const { return flat_box(nodes, id, &b); }
+  static double area(const Box& b) {
+    const double dx = b.mx[0] - b.mn[0], dy = b.mx[1] - b.mn[1], dz = b.mx[2] - b.mn[2];
+    return 2.0 * (dx * dy + dy * dz + dz * dx);
+  }
+
+  // Collapse the binary node `id` into one wide node: open the largest-area interior child until
+  // four children are reached or none is interior. Returns the wide id; *need = stack entries.
+  int build(int id, int depth, int* need) {
+    if (depth > 256) { ok = false; return 0; }
+    std::vector<int> kids{nodes[id].a, nodes[id].b};
+    for (;;) {
+      if ((int)kids.size() >= RT_WIDE) break;
+      int best = -1;
+      double best_area = -1;
+      for (int k = 0; k < (int)kids.size(); ++k) {
+        const rt_node& n = nodes[kids[k]];
+        if (n.type != RT_NODE_BVH) continue;
+        Box b;
+        if (!box_of(kids[k], b)) { ok = false; return 0; }
+        const double a = area(b);
+        if (a > best_area) { best_area = a; best = k; }
+      }
+      if (best < 0) break;
+      const rt_node& n = nodes[kids[best]];
+      kids[best] = n.a;
+      kids.insert(kids.begin() + best + 1, n.b);
+    }
+    const int me = (int)out.size();
+    out.push_back(rt_wnode{});
+    rt_wnode w{};
+    int child_need = 0;
+    for (int k = 0; k < RT_WIDE; ++k) {
+      if (k >= (int)kids.size()) {
+        for (int a = 0; a < 3; ++a) { w.lo[a][k] = INFINITY; w.hi[a][k] = -INFINITY; }
+        w.child[k] = RT_WIDE_EMPTY;
+        continue;
+      }
+      Box b;
+      if (!box_of(kids[k], b)) { ok = false; return 0; }
+      for (int a = 0; a < 3; ++a) { w.lo[a][k] = f32_down(b.mn[a]); w.hi[a][k] = f32_up(b.mx[a]); }
+      if (nodes[kids[k]].type == RT_NODE_BVH) {
+        int cn = 0;
+        w.child[k] = build(kids[k], depth + 1, &cn);
+        if (!ok) return 0;
+        child_need = std::max(child_need, cn);
+      } else {
+        w.child[k] = ~kids[k];
+      }
+    }
+    out[me] = w;
+    // the nearest hit child is entered, the other (<= 3) wait on the stack meanwhile
+    *need = (int)kids.size() - 1 + child_need;
+    return me;
+  }
+};
+
+}  // namespace
+
+// 4-wide collapse of the binary world tree at `root` (rebuilt or the reference's own). Returns
+// false when the root is not a BVH node or a box is not finite.
+bool build_wide_bvh(const std::vector<rt_node>& nodes, int root, std::vector<rt_wnode>& out, int* stack_need) {
+  out.clear();
+  *stack_need = 0;
+  if (root < 0 || root >= (int)nodes.size() || nodes[root].type != RT_NODE_BVH) return false;
+  WideBuilder b{nodes, out};
+  b.build(root, 0, stack_need);
+  if (!b.ok) {
+    out.clear();
+    return false;
+  }
+  return true;
 }
 
 }  // namespace rt

@@ -9,6 +9,7 @@
 #include <stdint.h>
 
 #include "rt.h"
+#include "rt_wide.h"
 
 #ifndef RT_BLOCK
 #define RT_BLOCK 128 /* threads per workgroup (2 waves) */
@@ -122,6 +123,7 @@ struct DMat {
 
 struct Scene {
   const rt_node* nodes;
+  const rt_wnode* wnodes;  // 4-wide world tree (F_WIDE kernels); null when not built
   const DMat* mats;
   const rt_texture* texs;
   const rt_perlin* perlins;

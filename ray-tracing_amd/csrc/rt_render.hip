@@ -30,6 +30,7 @@
 
 namespace rt {
 int rebuild_world_bvh(std::vector<rt_node>& nodes, int root);
+bool build_wide_bvh(const std::vector<rt_node>& nodes, int root, std::vector<rt_wnode>& out, int* stack_need);
 }
 
 using namespace rtd;
@@ -410,7 +411,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
         }
         continue;
       }
-      trav_begin(t, ray, S.world, INFINITY);
+      trav_begin<F>(t, ray, S.world, kEps, INFINITY);
       walking = true;
       if constexpr ((F & F_COUNT) != 0) ++segs;
     }
@@ -442,6 +443,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     wave_add(&A.work[4], cnt.light);
     wave_add(&A.work[5], blocks);
     wave_add(&A.work[6], samples);
+    wave_add(&A.work[7], cnt.wide);
     if ((threadIdx.x & 63) == 0) {
       atomicAdd(&A.work[8], ph_setup);
       atomicAdd(&A.work[9], ph_trav);
@@ -456,20 +458,25 @@ __global__ void __launch_bounds__(RT_BLOCK, WAVES) render_philox2(RenderArgs A) 
   philox_loop2<F>(A, A.S, &stk_mem[threadIdx.x], RT_BLOCK);
 }
 
+// LDS-staged replacement loop: the traversal's node array (the wide records for F_WIDE, else the
+// flat nodes) and the per-lane stacks live in the CU's LDS; leaves are read from global memory
+// under F_WIDE.
 template <unsigned F, int WAVES>
 __global__ void __launch_bounds__(WAVES * 256, WAVES) render_philox2_lds(RenderArgs A, int n_nodes, int stack_entries) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  rt_node* nodes = reinterpret_cast<rt_node*>(lds);
+  constexpr int rec = (F & F_WIDE) ? (int)sizeof(rt_wnode) : (int)sizeof(rt_node);
   {
-    const uint4* src = reinterpret_cast<const uint4*>(A.S.nodes);
+    const uint4* src = (F & F_WIDE) ? reinterpret_cast<const uint4*>(A.S.wnodes)
+                                    : reinterpret_cast<const uint4*>(A.S.nodes);
     uint4* dst = reinterpret_cast<uint4*>(lds);
-    const int n16 = n_nodes * (int)(sizeof(rt_node) / 16);
+    const int n16 = n_nodes * (rec / 16);
     for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
   }
   __syncthreads();
   Scene S = A.S;
-  S.nodes = nodes;
-  int* stk = reinterpret_cast<int*>(lds + (size_t)n_nodes * sizeof(rt_node)) + threadIdx.x;
+  if constexpr ((F & F_WIDE) != 0) S.wnodes = reinterpret_cast<const rt_wnode*>(lds);
+  else S.nodes = reinterpret_cast<const rt_node*>(lds);
+  int* stk = reinterpret_cast<int*>(lds + (size_t)n_nodes * rec) + threadIdx.x;
   (void)stack_entries;
   philox_loop2<F>(A, S, stk, WAVES * 256);
 }
@@ -530,8 +537,9 @@ __global__ void assemble(const T* slabs, T* image, int W, int H, int tile, int t
 }
 
 // ---------------------------------------------------------------- debug: closest hits
+template <unsigned F>
 __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* rays, int n, double tmin,
-                                                         double tmax, uint64_t seed, int joint, double* out) {
+                                                         double tmax, uint64_t seed, int joint, int walk, double* out) {
   __shared__ int stk_mem[RT_STACK * RT_BLOCK];
   int* stk = &stk_mem[threadIdx.x];
   const int i = blockIdx.x * RT_BLOCK + threadIdx.x;
@@ -542,8 +550,18 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
   g.init(seed, (uint32_t)i, 0);
   Hit h;
   double* o = out + 12 * (long long)i;
-  Cnt cnt{0, 0, 0, 0};
-  if (traverse<F_ALL | F_UV>(S, S.world, r, tmin, tmax, h, g, stk, joint != 0, cnt)) {
+  Cnt cnt{0, 0, 0, 0, 0};
+  bool got;
+  if (walk == 0) {
+    got = traverse<F>(S, S.world, r, tmin, tmax, h, g, stk, joint != 0, cnt);
+  } else {  // the render loop's resumable walk (binary, or 4-wide under F_WIDE)
+    Trav t;
+    trav_begin<F>(t, r, S.world, tmin, tmax);
+    while (trav_step<F>(S, t, tmin, stk, RT_BLOCK, joint != 0, cnt)) {
+    }
+    got = trav_finish<F>(S, t, r, tmin, h);
+  }
+  if (got) {
     o[0] = 1; o[1] = h.t;
     o[2] = h.p.x; o[3] = h.p.y; o[4] = h.p.z;
     o[5] = h.n.x; o[6] = h.n.y; o[7] = h.n.z;
@@ -595,6 +613,9 @@ struct rt_ctx {
   unsigned features = 0;
   int n_nodes = 0;
   int stack_need = 0;  // deepest traversal stack the world tree needs (entries)
+  rt_wnode* d_wnodes = nullptr;  // 4-wide world tree (replace_ok worlds with a BVH root)
+  int n_wnodes = 0;
+  int wide_stack_need = 0;
   bool rebuilt_bvh = false;
   bool replace_ok = false;  // media-free and no instance frames: the replacement loop applies
   bool has_scene = false;
@@ -630,6 +651,9 @@ void free_scene(rt_ctx* c) {
   (void)hipFree(c->d_perlins);
   (void)hipFree(c->d_images);
   (void)hipFree(c->d_pool);
+  (void)hipFree(c->d_wnodes);
+  c->d_wnodes = nullptr;
+  c->n_wnodes = 0;
   c->d_nodes = nullptr;
   c->d_mats = nullptr;
   c->d_texs = nullptr;
@@ -797,35 +821,44 @@ int waves_target(int dflt) {
   return (w >= 1 && w <= 4) ? w : dflt;
 }
 // Kernel pointer for (variant, replacement loop?, LDS-staged?, waves per SIMD, counting build?).
+// Kernel pointer for (variant, loop, LDS-staged?, waves per SIMD, counting build?); loop 0 = one
+// sample per lane walk, 1 = ray replacement over the binary tree, 2 = replacement over the
+// 4-wide tree.
 template <unsigned V>
-const void* pick(bool replace, bool lds, int w, bool count) {
-  if (count) return replace ? (const void*)render_philox2<V | F_COUNT, 1> : (const void*)render_philox<V | F_COUNT, 1>;
+const void* pick_w(bool lds, int w) {
   if (lds) {
-    if (replace) {
-      if (w == 2) return (const void*)render_philox2_lds<V, 2>;
-      if (w == 4) return (const void*)render_philox2_lds<V, 4>;
-      if (w == 1) return (const void*)render_philox2_lds<V, 1>;
-      return (const void*)render_philox2_lds<V, 3>;
-    }
+    if (w == 2) return (const void*)render_philox2_lds<V, 2>;
+    if (w == 4) return (const void*)render_philox2_lds<V, 4>;
+    if (w == 1) return (const void*)render_philox2_lds<V, 1>;
+    return (const void*)render_philox2_lds<V, 3>;
+  }
+  if (w == 2) return (const void*)render_philox2<V, 2>;
+  if (w == 3) return (const void*)render_philox2<V, 3>;
+  if (w == 4) return (const void*)render_philox2<V, 4>;
+  return (const void*)render_philox2<V, 1>;
+}
+template <unsigned V>
+const void* pick(int loop, bool lds, int w, bool count) {
+  if (count) {
+    if (loop == 2) return (const void*)render_philox2<V | F_WIDE | F_COUNT, 1>;
+    return loop ? (const void*)render_philox2<V | F_COUNT, 1> : (const void*)render_philox<V | F_COUNT, 1>;
+  }
+  if (loop == 2) return pick_w<V | F_WIDE>(lds, w);
+  if (loop == 1) return pick_w<V>(lds, w);
+  if (lds) {
     if (w == 2) return (const void*)render_philox_lds<V, 2>;
     if (w == 4) return (const void*)render_philox_lds<V, 4>;
     if (w == 1) return (const void*)render_philox_lds<V, 1>;
     return (const void*)render_philox_lds<V, 3>;
-  }
-  if (replace) {
-    if (w == 2) return (const void*)render_philox2<V, 2>;
-    if (w == 3) return (const void*)render_philox2<V, 3>;
-    if (w == 4) return (const void*)render_philox2<V, 4>;
-    return (const void*)render_philox2<V, 1>;
   }
   if (w == 2) return (const void*)render_philox<V, 2>;
   if (w == 3) return (const void*)render_philox<V, 3>;
   if (w == 4) return (const void*)render_philox<V, 4>;
   return (const void*)render_philox<V, 1>;
 }
-const void* philox_kernel(unsigned var, bool replace, bool lds, int w, bool count) {
-  if (var == kVarSpheres) return pick<kVarSpheres>(replace, lds, w, count);
-  if (var == kVarCornell) return pick<kVarCornell>(replace, lds, w, count);
+const void* philox_kernel(unsigned var, int loop, bool lds, int w, bool count) {
+  if (var == kVarSpheres) return pick<kVarSpheres>(loop, lds, w, count);
+  if (var == kVarCornell) return pick<kVarCornell>(loop, lds, w, count);
   return count ? (const void*)render_philox<F_ALL | F_COUNT, 1> : (const void*)render_philox<F_ALL, 1>;
 }
 bool env_off(const char* name) {
@@ -887,27 +920,33 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   A.trav_stop = stop_env ? std::max(0, std::min(63, std::atoi(stop_env))) : 16;
   const unsigned var = variant_for(c->features);
   const bool count = d_work != nullptr;
-  // Replacement loop for media-free worlds without instance frames (RTAMD_REPLACE=0 disables).
+  // Replacement loop for media-free worlds without instance frames (RTAMD_REPLACE=0 disables),
+  // over the 4-wide tree when one was built (RTAMD_WIDE=0 disables; the reference-cull flag
+  // asks for the binary tree's exact box test).
   const bool replace = c->replace_ok && var != F_ALL && !env_off("RTAMD_REPLACE");
+  const bool wide = replace && c->d_wnodes && !(p->flags & RT_FLAG_REFERENCE_CULL) && !env_off("RTAMD_WIDE");
+  const int loop = wide ? 2 : (replace ? 1 : 0);
   const int waves = var == kVarSpheres ? waves_target(3) : waves_target(1);
-  // LDS-staged kernel when the node array plus the traversal stack fit one CU's 160 KiB
+  // LDS-staged kernel when the traversal's node array plus the stacks fit one CU's 160 KiB
   // (RTAMD_LDS=0 disables it for A/B runs).
   if (!count && !env_off("RTAMD_LDS") && var != F_ALL) {
     const int block = waves * 256;
-    const int entries = c->stack_need + 2;
-    const size_t bytes = (size_t)c->n_nodes * sizeof(rt_node) + (size_t)entries * block * sizeof(int);
+    const int entries = (wide ? c->wide_stack_need : c->stack_need) + 2;
+    const int items = wide ? c->n_wnodes : c->n_nodes;
+    const size_t rec = wide ? sizeof(rt_wnode) : sizeof(rt_node);
+    const size_t bytes = (size_t)items * rec + (size_t)entries * block * sizeof(int);
     if (bytes <= 160 * 1024) {
-      const void* fn = philox_kernel(var, replace, true, waves, false);
+      const void* fn = philox_kernel(var, loop, true, waves, false);
       HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-      int n_nodes = c->n_nodes;
-      void* args[] = {&A, &n_nodes, (void*)&entries};
+      int n_items = items;
+      void* args[] = {&A, &n_items, (void*)&entries};
       HIPCHK(hipEventRecord(c->ev0, st));
       HIPCHK(hipLaunchKernel(fn, dim3(c->cu_count), dim3(block), args, bytes, st));
       HIPCHK(hipEventRecord(c->ev1, st));
       return RT_OK;
     }
   }
-  const void* fn = philox_kernel(var, replace, false, count ? 1 : waves, count);
+  const void* fn = philox_kernel(var, loop, false, count ? 1 : waves, count);
   int bpc = 1;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, RT_BLOCK, 0));
   const long long want = (slab + RT_BLOCK - 1) / RT_BLOCK;
@@ -1045,6 +1084,20 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
     if (((x.type & RT_TYPE_MASK) == RT_NODE_TRANSLATE || (x.type & RT_TYPE_MASK) == RT_NODE_ROTATE) &&
         !(x.type & RT_CHAIN_PRIM))
       c->replace_ok = false;
+  if (c->replace_ok) {  // 4-wide fp32-box tree over the same world tree (unflagged node copy)
+    std::vector<rt_wnode> wide;
+    int need = 0;
+    if (rt::build_wide_bvh(nodes, d->world_root, wide, &need) && need + 2 <= RT_STACK) {
+      if ((rc = upload(&c->d_wnodes, wide.data(), wide.size()))) {
+        free_scene(c);
+        return rc;
+      }
+      c->n_wnodes = (int)wide.size();
+      c->wide_stack_need = need;
+      S.wnodes = c->d_wnodes;
+    }
+  }
+  if (!c->d_wnodes) S.wnodes = nullptr;
   c->has_scene = true;
   return RT_OK;
 }
@@ -1225,14 +1278,24 @@ int rt_debug_closest_hits(rt_ctx* c, const double* rays, int n, double tmin, dou
     rt::set_error("rt_debug_closest_hits: no scene uploaded");
     return RT_E_STATE;
   }
+  if ((flags & (RT_DEBUG_RESUMABLE | RT_DEBUG_WIDE)) && !c->replace_ok)
+    return unsupported("rt_debug_closest_hits: the resumable walks need a world without media and frames");
+  if ((flags & RT_DEBUG_WIDE) && !c->d_wnodes)
+    return unsupported("rt_debug_closest_hits: no 4-wide tree for this world");
   if (n == 0) return RT_OK;
   HIPCHK(hipSetDevice(c->device));
   double *d_rays = nullptr, *d_out = nullptr;
   HIPCHK(hipMalloc((void**)&d_rays, sizeof(double) * 7 * (size_t)n));
   HIPCHK(hipMalloc((void**)&d_out, sizeof(double) * 12 * (size_t)n));
   HIPCHK(hipMemcpy(d_rays, rays, sizeof(double) * 7 * (size_t)n, hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(closest_hits, dim3((n + RT_BLOCK - 1) / RT_BLOCK), dim3(RT_BLOCK), 0, c->stream, c->scene,
-                     d_rays, n, tmin, tmax, seed, (int)!(flags & RT_FLAG_REFERENCE_CULL), d_out);
+  const int joint = !(flags & RT_FLAG_REFERENCE_CULL);
+  const dim3 grid((n + RT_BLOCK - 1) / RT_BLOCK);
+  if (flags & RT_DEBUG_WIDE)
+    hipLaunchKernelGGL(closest_hits<F_ALL | F_UV | F_WIDE>, grid, dim3(RT_BLOCK), 0, c->stream, c->scene, d_rays, n,
+                       tmin, tmax, seed, joint, 1, d_out);
+  else
+    hipLaunchKernelGGL(closest_hits<F_ALL | F_UV>, grid, dim3(RT_BLOCK), 0, c->stream, c->scene, d_rays, n, tmin,
+                       tmax, seed, joint, (flags & RT_DEBUG_RESUMABLE) ? 1 : 0, d_out);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipMemcpy(out, d_out, sizeof(double) * 12 * (size_t)n, hipMemcpyDeviceToHost));

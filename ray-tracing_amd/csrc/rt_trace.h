@@ -14,12 +14,13 @@ enum : unsigned {
   F_TEX = 32u,    // Checker / Perlin / Image textures (and sphere u, v)
   F_ALL = 63u,
   F_UV = 64u,     // always compute sphere (u, v) (debug queries)
-  F_COUNT = 128u  // counting build: per-lane work counters (DESIGN.md "Roofline")
+  F_COUNT = 128u, // counting build: per-lane work counters (DESIGN.md "Roofline")
+  F_WIDE = 256u   // resumable walk over the 4-wide fp32-box tree (rt_wide.h) instead of the binary one
 };
 
 // Work counters of the counting build (F_COUNT); all zero-cost otherwise.
 struct Cnt {
-  unsigned box, prim, other, light;
+  unsigned box, prim, other, light, wide;
 };
 
 // ------------------------------------------------------------------ textures (Lib.hs:441-513)
@@ -494,9 +495,24 @@ struct Trav {
   double closest;    // current bound (closest hit so far)
   double best_tmax;  // chain hits: the bound in force when the best hit was found
   int node, sp, best_node, best_sub;
+  // F_WIDE: the ray in fp32 for the conservative child-box test (wide_children)
+  float o32x, o32y, o32z, i32x, i32y, i32z;
+  float slack, tmin32, tmax32;
+  unsigned oct;   // bit a: the ray runs towards -axis a (its near plane is the box's hi)
+  bool all;       // a direction component too small for fp32: accept every child
 };
 
-__device__ __forceinline__ void trav_begin(Trav& t, const Ray& r, int root, double t_max) {
+__device__ __forceinline__ float f32_lower(double x) {  // <= x (or -inf)
+  const float f = (float)x;
+  return f - fabsf(f) * 0x1p-22f;
+}
+__device__ __forceinline__ float f32_upper(double x) {  // >= x (or +inf)
+  const float f = (float)x;
+  return f + fabsf(f) * 0x1p-22f;
+}
+
+template <unsigned F>
+__device__ __forceinline__ void trav_begin(Trav& t, const Ray& r, int root, double t_min, double t_max) {
   t.ray = prep(r);
   t.closest = t_max;
   t.best_tmax = t_max;
@@ -504,31 +520,45 @@ __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r, int root, doub
   t.sp = 0;
   t.best_node = -1;
   t.best_sub = 0;
+  if constexpr ((F & F_WIDE) != 0) {
+    t.node = 0;  // wide root
+    t.o32x = (float)r.o.x;
+    t.o32y = (float)r.o.y;
+    t.o32z = (float)r.o.z;
+    t.i32x = (float)t.ray.inv.x;
+    t.i32y = (float)t.ray.inv.y;
+    t.i32z = (float)t.ray.inv.z;
+    // K = max |o * (1/d)| over the finite axes (the origin's rounding, in t units)
+    const float kx = isinf(t.i32x) ? 0.0f : fabsf(t.o32x * t.i32x);
+    const float ky = isinf(t.i32y) ? 0.0f : fabsf(t.o32y * t.i32y);
+    const float kz = isinf(t.i32z) ? 0.0f : fabsf(t.o32z * t.i32z);
+    t.slack = fmaxf(fmaxf(kx, ky), kz) * 0x1p-20f;
+    t.tmin32 = f32_lower(t_min);
+    t.tmax32 = f32_upper(t_max);
+    t.oct = (signbit(t.i32x) ? 1u : 0u) | (signbit(t.i32y) ? 2u : 0u) | (signbit(t.i32z) ? 4u : 0u);
+    // 1/d overflowing fp32 for d != 0 (|d| < 2^-126), a NaN direction or a non-finite origin:
+    // the fp32 distances say nothing, every child is entered (the leaves still decide exactly)
+    const bool bad = (isinf(t.i32x) & (r.d.x != 0.0)) | (isinf(t.i32y) & (r.d.y != 0.0)) |
+                     (isinf(t.i32z) & (r.d.z != 0.0)) | isnan(t.i32x) | isnan(t.i32y) | isnan(t.i32z) |
+                     !isfinite(t.o32x) | !isfinite(t.o32y) | !isfinite(t.o32z) | isnan(t.slack);
+    t.all = bad;
+  }
 }
 
-// Visit one node; false once the walk is over.
+// Leaf of the resumable walk (a primitive, or an instance chain ending in one).
 template <unsigned F>
-__device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min, int* stk, int stride, bool joint,
-                                          Cnt& cnt) {
-  const rt_node* n = &S.nodes[t.node];
+__device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, int id, double t_min, Cnt& cnt) {
+  const rt_node* n = &S.nodes[id];
   const int type = n->type & RT_TYPE_MASK;
-  if (type == RT_NODE_BVH) {
-    if constexpr ((F & F_COUNT) != 0) ++cnt.box;
-    if (box_hit(n->f, t.ray, t_min, t.closest, joint)) {
-      const int c = n->c;
-      const bool flip = (c & RT_BVH_ORDERED) && comp(t.ray.d, c & 3) < 0;
-      stk[(t.sp++) * stride] = flip ? n->a : n->b;
-      t.node = flip ? n->b : n->a;
-      return true;
-    }
-  } else if ((F & F_INST) && (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE)) {
+  if ((F & F_INST) && (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE)) {
     if constexpr ((F & F_COUNT) != 0) ++cnt.other;
     Hit h;
-    if (chain_hit<F>(S, t.node, plain(t.ray), t_min, t.closest, h)) {
+    if (chain_hit<F>(S, id, plain(t.ray), t_min, t.closest, h)) {
       t.best_tmax = t.closest;
       t.closest = h.t;
-      t.best_node = t.node;
+      t.best_node = id;
       t.best_sub = -1;
+      if constexpr ((F & F_WIDE) != 0) t.tmax32 = f32_upper(t.closest);
     }
   } else {
     if constexpr ((F & F_COUNT) != 0) ++cnt.prim;
@@ -536,8 +566,98 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
     int sub;
     if (prim_t<F>(S, n, t.ray, t_min, t.closest, tt, sub)) {
       t.closest = tt;
-      t.best_node = t.node;
+      t.best_node = id;
       t.best_sub = sub;
+      if constexpr ((F & F_WIDE) != 0) t.tmax32 = f32_upper(t.closest);
+    }
+  }
+}
+
+// Conservative fp32 slab test of one child box (the rows hold the near / far planes per axis).
+// Each plane distance (plane - o32) * i32 is within eps*(K + 3|t|) of the exact distance to the
+// fp32 box (eps = 2^-24, K = max |o * (1/d)| over finite axes); the test accepts when
+// near - far <= 2^-20 * (max(|near|, |far|) + K), so it accepts every ray whose exact slab interval
+// over the box is non-empty, and the fp32 box contains the fp64 one. A zero direction component
+// gives i32 = +-inf: its distances are +-inf (origin outside the slab: the ray misses, or the
+// axis does not constrain), or NaN exactly when the origin lies on the plane, which fmaxf/fminf
+// (IEEE maxNum/minNum) drop — the plane then does not constrain, as for a ray inside the slab.
+__device__ __forceinline__ float wide_key(const Trav& t, float nx, float ny, float nz, float fx, float fy, float fz,
+                                          int child) {
+  const float tnx = (nx - t.o32x) * t.i32x, tny = (ny - t.o32y) * t.i32y, tnz = (nz - t.o32z) * t.i32z;
+  const float tfx = (fx - t.o32x) * t.i32x, tfy = (fy - t.o32y) * t.i32y, tfz = (fz - t.o32z) * t.i32z;
+  const float near = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, t.tmin32));
+  const float far = fminf(fminf(tfx, tfy), fminf(tfz, t.tmax32));
+  const bool hit = ((near - far <= fmaf(fmaxf(fabsf(near), fabsf(far)), 0x1p-20f, t.slack)) | t.all) &
+                   (child != RT_WIDE_EMPTY);
+  return hit ? fminf(near, 3.0e38f) : INFINITY;
+}
+
+__device__ __forceinline__ void cswap(float& ka, int& ca, float& kb, int& cb) {
+  const bool s = kb < ka;
+  const float k = s ? kb : ka;
+  const int c = s ? cb : ca;
+  kb = s ? ka : kb;
+  cb = s ? ca : cb;
+  ka = k;
+  ca = c;
+}
+
+// One wide node: test the four child boxes, enter the nearest accepted child, stack the others
+// (farthest deepest).
+__device__ __forceinline__ bool wide_node(const Scene& S, Trav& t, int* stk, int stride) {
+  const float* base = reinterpret_cast<const float*>(&S.wnodes[t.node]);
+  const int ox = (t.oct & 1u) ? 12 : 0, oy = (t.oct & 2u) ? 16 : 4, oz = (t.oct & 4u) ? 20 : 8;
+  const float4 nx = *reinterpret_cast<const float4*>(base + ox);
+  const float4 ny = *reinterpret_cast<const float4*>(base + oy);
+  const float4 nz = *reinterpret_cast<const float4*>(base + oz);
+  const float4 fx = *reinterpret_cast<const float4*>(base + (ox ^ 12));
+  const float4 fy = *reinterpret_cast<const float4*>(base + (oy < 12 ? oy + 12 : oy - 12));
+  const float4 fz = *reinterpret_cast<const float4*>(base + (oz < 12 ? oz + 12 : oz - 12));
+  const int4 ch = *reinterpret_cast<const int4*>(base + 24);
+  float k0 = wide_key(t, nx.x, ny.x, nz.x, fx.x, fy.x, fz.x, ch.x);
+  float k1 = wide_key(t, nx.y, ny.y, nz.y, fx.y, fy.y, fz.y, ch.y);
+  float k2 = wide_key(t, nx.z, ny.z, nz.z, fx.z, fy.z, fz.z, ch.z);
+  float k3 = wide_key(t, nx.w, ny.w, nz.w, fx.w, fy.w, fz.w, ch.w);
+  int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
+  const int n_hit = (k0 < INFINITY) + (k1 < INFINITY) + (k2 < INFINITY) + (k3 < INFINITY);
+  cswap(k0, c0, k1, c1);
+  cswap(k2, c2, k3, c3);
+  cswap(k0, c0, k2, c2);
+  cswap(k1, c1, k3, c3);
+  cswap(k1, c1, k2, c2);
+  if (n_hit == 0) return false;
+  if (n_hit > 3) stk[(t.sp++) * stride] = c3;
+  if (n_hit > 2) stk[(t.sp++) * stride] = c2;
+  if (n_hit > 1) stk[(t.sp++) * stride] = c1;
+  t.node = c0;
+  return true;
+}
+
+// Visit one node; false once the walk is over.
+template <unsigned F>
+__device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min, int* stk, int stride, bool joint,
+                                          Cnt& cnt) {
+  if constexpr ((F & F_WIDE) != 0) {
+    if (t.node >= 0) {
+      if constexpr ((F & F_COUNT) != 0) ++cnt.wide;
+      if (wide_node(S, t, stk, stride)) return true;
+    } else {
+      trav_leaf<F>(S, t, ~t.node, t_min, cnt);
+    }
+  } else {
+    const rt_node* n = &S.nodes[t.node];
+    const int type = n->type & RT_TYPE_MASK;
+    if (type == RT_NODE_BVH) {
+      if constexpr ((F & F_COUNT) != 0) ++cnt.box;
+      if (box_hit(n->f, t.ray, t_min, t.closest, joint)) {
+        const int c = n->c;
+        const bool flip = (c & RT_BVH_ORDERED) && comp(t.ray.d, c & 3) < 0;
+        stk[(t.sp++) * stride] = flip ? n->a : n->b;
+        t.node = flip ? n->b : n->a;
+        return true;
+      }
+    } else {
+      trav_leaf<F>(S, t, t.node, t_min, cnt);
     }
   }
   if (t.sp == 0) return false;

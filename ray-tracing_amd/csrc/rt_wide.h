@@ -1,0 +1,25 @@
+// rt_wide.h — the device's 4-wide BVH record (internal; shared by the host builder in rt_bvh.cpp
+// and the traversal in rt_trace.h). Not part of the C ABI: rt_upload_scene derives it from the
+// flattened world tree when the world holds no ConstantMedium and no instance frames.
+//
+// One record is 128 bytes = one LDS/L2 line pair: four child boxes as single-precision rows
+// (lo[axis][child], hi[axis][child]), rounded OUTWARD from the fp64 boxes so that each box
+// contains the double-precision one, then four child references. The fp32 test over these boxes
+// only culls (it accepts every ray the fp64 slab test over the same boxes accepts, see
+// wide_children in rt_trace.h); every leaf is still hit-tested in fp64 exactly as the reference.
+#pragma once
+#include <stdint.h>
+
+#define RT_WIDE 4
+#define RT_WIDE_EMPTY ((int32_t)0x80000000)  // unused child slot (its box is empty: lo = +inf, hi = -inf)
+
+typedef struct rt_wnode {
+  float lo[3][RT_WIDE];
+  float hi[3][RT_WIDE];
+  int32_t child[RT_WIDE];  // >= 0: wide node id; < 0: leaf, ~child = flat rt_node id; RT_WIDE_EMPTY
+  int32_t pad[RT_WIDE];
+} rt_wnode;
+
+#ifdef __cplusplus
+static_assert(sizeof(rt_wnode) == 128, "rt_wnode is 128 bytes");
+#endif

@@ -32,6 +32,8 @@ RT_RNG_EXACT, RT_RNG_PHILOX = 0, 1
 RT_FLAG_NAN_CULL = 1
 RT_FLAG_REFERENCE_CULL = 2
 RT_UPLOAD_REFERENCE_BVH = 1
+RT_DEBUG_RESUMABLE = 4  # rt_debug_closest_hits: the render loop's resumable binary walk
+RT_DEBUG_WIDE = 8       # rt_debug_closest_hits: the resumable walk over the 4-wide fp32-box tree
 RT_BVH_ORDERED = 0x40000000
 MATH_OPS = {"div": 0, "div_exact": 1, "sqrt": 2, "sin": 3, "cos": 4, "atan": 5, "asin": 6, "log": 7, "pow": 8,
             "ghc_atan2": 9, "tan": 10}
@@ -458,13 +460,14 @@ class Context:
         _check(lib().rt_assemble_linear_async(self._h, C.byref(params), C.c_void_p(d_slabs), C.c_void_p(d_image),
                                               C.c_void_p(stream or None)), "rt_assemble_linear_async")
 
-    WORK_FIELDS = ("segments", "box_tests", "prim_tests", "other_tests", "light_pdfs", "philox_blocks", "samples")
+    WORK_FIELDS = ("segments", "box_tests", "prim_tests", "other_tests", "light_pdfs", "philox_blocks", "samples",
+                   "wide_nodes")
 
     def render_work(self, cam, params) -> dict:
         """Device-measured work of one tier-B render (counting build): totals per field."""
         w = (C.c_uint64 * 16)()
         _check(lib().rt_render_work(self._h, C.byref(cam), C.byref(params), w), "rt_render_work")
-        out = dict(zip(self.WORK_FIELDS, [int(x) for x in w[:7]]))
+        out = dict(zip(self.WORK_FIELDS, [int(x) for x in w[:8]]))
         tot = max(1, int(w[8]) + int(w[9]) + int(w[10]))
         out["phase_split"] = {"acquire_camera": int(w[8]) / tot, "traverse": int(w[9]) / tot, "shade": int(w[10]) / tot}
         return out

@@ -129,6 +129,83 @@ def test_closest_hits_bit_exact(gpu_ctx, name, flags):
     assert full >= 0.95
 
 
+def _special_rays(sc, rng, n):
+    """Rays that stress a conservative box test: origins exactly on sphere bounding-box planes,
+    axis-aligned directions (exact zeros, both signs: the light-sample direction (1,0,0) of the
+    NaN quirk), direction components far below fp32 range, and long grazing rays."""
+    nodes = sc.nodes
+    sph = nodes[nodes["type"] == rtamd.RT_NODE_SPHERE]
+    c = sph["f"][:, :3]
+    rad = sph["f"][:, 3]
+    k = rng.integers(0, len(sph), n)
+    axis = rng.integers(0, 3, n)
+    sign = rng.choice([-1.0, 1.0], n)
+    o = c[k].copy()
+    o[np.arange(n), axis] += sign * rad[k]                      # on the box face (and the sphere)
+    o += rng.normal(0, 1, (n, 3)) * (rng.random((n, 1)) < 0.5)  # half of them moved off it
+    d = np.zeros((n, 3))
+    kind = rng.integers(0, 4, n)
+    ax2 = rng.integers(0, 3, n)
+    d[np.arange(n), ax2] = rng.choice([-1.0, 1.0], n)           # axis-aligned
+    m = kind == 1
+    d[m] = rng.normal(0, 1, (m.sum(), 3))
+    d[m, ax2[m]] = rng.choice([0.0, -0.0, 1e-40, -1e-300], m.sum())  # one tiny or signed-zero component
+    m = kind == 2
+    d[m] = np.array([1.0, 0.0, 0.0])                           # htblRandom's Unhittable direction
+    m = kind == 3
+    d[m] = rng.normal(0, 1, (m.sum(), 3))
+    return np.concatenate([o, d, rng.uniform(0, 1, (n, 1))], axis=1)
+
+
+@pytest.mark.parametrize("walk", [rtamd.RT_DEBUG_RESUMABLE, rtamd.RT_DEBUG_WIDE])
+@pytest.mark.parametrize("name", ["random_book_one", "three_spheres", "cornell", "stress_spheres"])
+def test_resumable_walks_closest_hits(gpu_ctx, name, walk):
+    """The render loop's walks (binary resumable; 4-wide with conservative fp32 child boxes) give
+    the oracle's closest hits (the reference's makeBVH tree, fp64 slab tests) on random and
+    adversarial rays: same primitive, t, p, normal bit-identical."""
+    sc, _ = _scene(name, param=3000 if name == "stress_spheres" else 0)
+    gpu_ctx.upload(sc)
+    rng = np.random.default_rng(17)
+    n = 1 << 15
+    if name == "cornell":
+        o = rng.uniform(20, 530, (n, 3))
+        d = rng.normal(0, 1, (n, 3))
+        d[: n // 4] = np.eye(3)[rng.integers(0, 3, n // 4)] * rng.choice([-1.0, 1.0], (n // 4, 1))
+        rays = np.concatenate([o, d, rng.uniform(0, 1, (n, 1))], axis=1)
+    else:
+        o = np.array([13.0, 2.0, 3.0]) + rng.normal(0, 0.5, (n, 3))
+        d = np.array([-13.0, -2.0, -3.0]) + rng.normal(0, 3.0, (n, 3))
+        rays = np.concatenate([np.concatenate([o, d, rng.uniform(0, 1, (n, 1))], axis=1),
+                               _special_rays(sc, rng, n)])
+    got = gpu_ctx.closest_hits(rays, 1e-4, np.inf, seed=3, flags=walk)
+    ref = pyoracle.closest_hits(sc, rays, 1e-4, np.inf, seed=3)
+    assert got[:, 0].sum() > len(rays) // 8
+    bad = ~np.all(got[:, [0, 1, 2, 3, 4, 5, 6, 7, 10, 11]] == ref[:, [0, 1, 2, 3, 4, 5, 6, 7, 10, 11]], axis=1)
+    if bad.any():
+        import os
+        os.makedirs("gpurun_out", exist_ok=True)
+        np.savez(f"gpurun_out/walk_{name}_{walk}.npz", rays=rays[bad], got=got[bad], ref=ref[bad])
+    assert not bad.any(), f"{int(bad.sum())} of {len(rays)} rays differ"
+    assert np.all(np.abs(got[:, 8:10] - ref[:, 8:10]) <= 4e-16)
+
+
+@pytest.mark.parametrize("name,cam", [("random_book_one", "random_scene"), ("cornell", "cornell")])
+def test_walks_output_identical(gpu_ctx, name, cam, monkeypatch):
+    """Full tier-B images: 4-wide walk == binary replacement walk == one-sample-per-lane loop,
+    byte for byte and in the linear averages (the walks differ only in which boxes they cull)."""
+    sc, _ = _scene(name)
+    c = rtamd.camera(cam, 160, 96)
+    gpu_ctx.upload(sc)
+    p = rtamd.make_params(160, 96, 4, 50, rtamd.RT_RNG_PHILOX, seed=5)
+    rgb_w, lin_w, _ = gpu_ctx.render(c, p, linear=True)
+    monkeypatch.setenv("RTAMD_WIDE", "0")
+    rgb_b, lin_b, _ = gpu_ctx.render(c, p, linear=True)
+    monkeypatch.setenv("RTAMD_REPLACE", "0")
+    rgb_s, lin_s, _ = gpu_ctx.render(c, p, linear=True)
+    assert np.array_equal(rgb_w, rgb_b) and np.array_equal(rgb_w, rgb_s)
+    assert np.array_equal(lin_w, lin_b, equal_nan=True) and np.array_equal(lin_w, lin_s, equal_nan=True)
+
+
 def test_shard_invariance(gpu_ctx):
     """Tier B output is byte-identical for any shard count (tiles dealt round-robin)."""
     import ctypes as C
