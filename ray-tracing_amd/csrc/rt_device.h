@@ -130,6 +130,7 @@ struct Scene {
   const rt_image* images;
   const uint8_t* pool;
   int world;
+  int world_ref;  // the caller's (makeBVH) world root: exact ties are resolved on this tree
   int lights;
   double bg[3];
 };

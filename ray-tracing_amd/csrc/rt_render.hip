@@ -339,6 +339,11 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     unsigned long long s0 = 0;
     if constexpr ((F & F_COUNT) != 0) s0 = stamp();
     // ---- shade finished walks, then set up the next walk for every lane that is not walking
+    if (ready && t.tie) {  // exact tie: redo this walk as the reference does
+      ready = false;
+      trav_restart_ref(t, S.world_ref, INFINITY);
+      walking = true;
+    }
     if (ready) {
       ready = false;
       Hit h;
@@ -489,6 +494,9 @@ template <unsigned F>
 __global__ void __launch_bounds__(RT_BLOCK) render_exact(RenderArgs A) {
   __shared__ int stk_mem[RT_STACK * RT_BLOCK];
   int* stk = &stk_mem[threadIdx.x];
+  // Tier A reproduces the reference's stream exactly, exact ties included: walk the caller's tree.
+  Scene S = A.S;
+  S.world = S.world_ref;
   const int x = blockIdx.x * RT_BLOCK + threadIdx.x;
   if (x >= A.W) return;
   RngExact g{A.gens[2 * x], A.gens[2 * x + 1]};
@@ -508,7 +516,7 @@ __global__ void __launch_bounds__(RT_BLOCK) render_exact(RenderArgs A) {
       V3 thr = v3(1.0, 1.0, 1.0), contrib;
       int depth = A.max_depth;
       Cnt cnt{0, 0, 0, 0};
-      while (!segment<F>(A, A.S, ray, thr, depth, g, stk, contrib, cnt)) {
+      while (!segment<F>(A, S, ray, thr, depth, g, stk, contrib, cnt)) {
       }
       sum = sum + contrib;
     }
@@ -558,6 +566,11 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
     Trav t;
     trav_begin<F>(t, r, S.world, tmin, tmax);
     while (trav_step<F>(S, t, tmin, stk, RT_BLOCK, joint != 0, cnt)) {
+    }
+    if (t.tie) {
+      trav_restart_ref(t, S.world_ref, tmax);
+      while (trav_step<F>(S, t, tmin, stk, RT_BLOCK, joint != 0, cnt)) {
+      }
     }
     got = trav_finish<F>(S, t, r, tmin, h);
   }
@@ -1023,7 +1036,13 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
       rt::set_error("rt_upload_scene: " + v0.err);
       return v0.code;
     }
-    dd.world_root = rt::rebuild_world_bvh(nodes, din->world_root);
+    // Only for worlds the replacement loop walks (no instance frames; media are refused by the
+    // rebuild itself): their walks resolve exact ties on the caller's tree (trav_finish).
+    bool frames = false;
+    for (const rt_node& x : v0.nodes)
+      frames |= ((x.type & RT_TYPE_MASK) == RT_NODE_TRANSLATE || (x.type & RT_TYPE_MASK) == RT_NODE_ROTATE) &&
+                !(x.type & RT_CHAIN_PRIM);
+    if (!frames) dd.world_root = rt::rebuild_world_bvh(nodes, din->world_root);
   }
   dd.nodes = nodes.data();
   dd.n_nodes = (int)nodes.size();
@@ -1074,11 +1093,13 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
   S.images = c->d_images;
   S.pool = c->d_pool;
   S.world = d->world_root;
+  S.world_ref = din->world_root;
   S.lights = d->lights_root;
   for (int i = 0; i < 3; ++i) S.bg[i] = d->background[i];
   c->features = scene_features(d);
   c->n_nodes = d->n_nodes;
-  c->stack_need = v.stack_need[d->world_root];
+  // (tie redo walks the caller's tree: size the stacks for both)
+  c->stack_need = std::max(v.stack_need[d->world_root], v.stack_need[din->world_root]);
   c->replace_ok = !(c->features & F_MEDIA);
   for (const rt_node& x : v.nodes)
     if (((x.type & RT_TYPE_MASK) == RT_NODE_TRANSLATE || (x.type & RT_TYPE_MASK) == RT_NODE_ROTATE) &&
@@ -1087,13 +1108,14 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
   if (c->replace_ok) {  // 4-wide fp32-box tree over the same world tree (unflagged node copy)
     std::vector<rt_wnode> wide;
     int need = 0;
-    if (rt::build_wide_bvh(nodes, d->world_root, wide, &need) && need + 2 <= RT_STACK) {
+    if (rt::build_wide_bvh(nodes, d->world_root, wide, &need) && need + 2 <= RT_STACK &&
+        (size_t)wide.size() < (size_t)INT32_MAX / 2) {
       if ((rc = upload(&c->d_wnodes, wide.data(), wide.size()))) {
         free_scene(c);
         return rc;
       }
       c->n_wnodes = (int)wide.size();
-      c->wide_stack_need = need;
+      c->wide_stack_need = std::max(need, v.stack_need[din->world_root]);
       S.wnodes = c->d_wnodes;
     }
   }

@@ -492,9 +492,12 @@ __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr
 // lanes whose walk has ended are shaded and restarted while the others keep walking.
 struct Trav {
   RayX ray;
-  double closest;    // current bound (closest hit so far)
-  double best_tmax;  // chain hits: the bound in force when the best hit was found
+  double closest;     // closest hit so far
+  double closest_up;  // the test bound: next double above `closest`, so that exact ties are seen
+  double best_tmax;   // chain hits: the bound in force when the best hit was found
   int node, sp, best_node, best_sub;
+  bool tie;           // a second leaf hit at exactly `closest`: the walk is redone with `ref`
+  bool ref;           // the reference's own walk: caller's tree, left first, bound = closest
   // F_WIDE: the ray in fp32 for the conservative child-box test (wide_children)
   float o32x, o32y, o32z, i32x, i32y, i32z;
   float slack, tmin32, tmax32;
@@ -515,11 +518,14 @@ template <unsigned F>
 __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r, int root, double t_min, double t_max) {
   t.ray = prep(r);
   t.closest = t_max;
+  t.closest_up = nextafter(t_max, INFINITY);
   t.best_tmax = t_max;
   t.node = root;
   t.sp = 0;
   t.best_node = -1;
   t.best_sub = 0;
+  t.tie = false;
+  t.ref = false;
   if constexpr ((F & F_WIDE) != 0) {
     t.node = 0;  // wide root
     t.o32x = (float)r.o.x;
@@ -545,7 +551,40 @@ __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r, int root, doub
   }
 }
 
-// Leaf of the resumable walk (a primitive, or an instance chain ending in one).
+// Redo the walk as the reference does it: the caller's tree, left child first (its nodes carry
+// no RT_BVH_ORDERED), every accepted hit replacing the best under bound = closest.
+__device__ __forceinline__ void trav_restart_ref(Trav& t, int root, double t_max) {
+  t.node = root;
+  t.sp = 0;
+  t.closest = t_max;
+  t.closest_up = t_max;
+  t.best_tmax = t_max;
+  t.best_node = -1;
+  t.best_sub = 0;
+  t.tie = false;
+  t.ref = true;
+}
+
+// Leaf of the resumable walk (a primitive, or an instance chain ending in one). Leaves are tested
+// under the bound closest_up, so a hit at exactly `closest` is seen: the reference keeps the
+// first such leaf in its tree's depth-first order unless a later one accepts t == tmax (rects,
+// Lib.hs:1005-1028, vs spheres' strict t < tmax), an order this walk does not follow — such a
+// tie is flagged, and the caller redoes the walk as the reference does it (trav_restart_ref).
+// Exact ties need two surfaces through one point on the ray (e.g. the book-one glass sphere
+// resting on the ground at (0,0,0)); they are rare, so the redo costs nothing measurable.
+template <unsigned F>
+__device__ __forceinline__ void trav_take(Trav& t, double x, int id, int sub) {
+  if (t.ref || x < t.closest) {  // (ref: every accepted hit replaces, as hit BVHNode prefers the right one)
+    t.best_tmax = t.closest_up;
+    t.closest = x;
+    t.closest_up = t.ref ? x : nextafter(x, INFINITY);
+    t.best_node = id;
+    t.best_sub = sub;
+    if constexpr ((F & F_WIDE) != 0) t.tmax32 = f32_upper(x);
+  } else if (x == t.closest) {
+    t.tie = true;
+  }
+}
 template <unsigned F>
 __device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, int id, double t_min, Cnt& cnt) {
   const rt_node* n = &S.nodes[id];
@@ -553,23 +592,12 @@ __device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, int id, doubl
   if ((F & F_INST) && (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE)) {
     if constexpr ((F & F_COUNT) != 0) ++cnt.other;
     Hit h;
-    if (chain_hit<F>(S, id, plain(t.ray), t_min, t.closest, h)) {
-      t.best_tmax = t.closest;
-      t.closest = h.t;
-      t.best_node = id;
-      t.best_sub = -1;
-      if constexpr ((F & F_WIDE) != 0) t.tmax32 = f32_upper(t.closest);
-    }
+    if (chain_hit<F>(S, id, plain(t.ray), t_min, t.closest_up, h)) trav_take<F>(t, h.t, id, -1);
   } else {
     if constexpr ((F & F_COUNT) != 0) ++cnt.prim;
     double tt;
     int sub;
-    if (prim_t<F>(S, n, t.ray, t_min, t.closest, tt, sub)) {
-      t.closest = tt;
-      t.best_node = id;
-      t.best_sub = sub;
-      if constexpr ((F & F_WIDE) != 0) t.tmax32 = f32_upper(t.closest);
-    }
+    if (prim_t<F>(S, n, t.ray, t_min, t.closest_up, tt, sub)) trav_take<F>(t, tt, id, sub);
   }
 }
 
@@ -587,8 +615,9 @@ __device__ __forceinline__ float wide_key(const Trav& t, float nx, float ny, flo
   const float tfx = (fx - t.o32x) * t.i32x, tfy = (fy - t.o32y) * t.i32y, tfz = (fz - t.o32z) * t.i32z;
   const float near = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, t.tmin32));
   const float far = fminf(fminf(tfx, tfy), fminf(tfz, t.tmax32));
-  const bool hit = ((near - far <= fmaf(fmaxf(fabsf(near), fabsf(far)), 0x1p-20f, t.slack)) | t.all) &
-                   (child != RT_WIDE_EMPTY);
+  // (an infinite near or far — a parallel ray outside the slab — must not widen the margin)
+  const float mag = fminf(fmaxf(fabsf(near), fabsf(far)), 3.0e38f);
+  const bool hit = ((near - far <= fmaf(mag, 0x1p-20f, t.slack)) | t.all) & (child != RT_WIDE_EMPTY);
   return hit ? fminf(near, 3.0e38f) : INFINITY;
 }
 
@@ -637,7 +666,9 @@ __device__ __forceinline__ bool wide_node(const Scene& S, Trav& t, int* stk, int
 template <unsigned F>
 __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min, int* stk, int stride, bool joint,
                                           Cnt& cnt) {
-  if constexpr ((F & F_WIDE) != 0) {
+  bool wide = false;
+  if constexpr ((F & F_WIDE) != 0) wide = !t.ref;
+  if (wide) {
     if (t.node >= 0) {
       if constexpr ((F & F_COUNT) != 0) ++cnt.wide;
       if (wide_node(S, t, stk, stride)) return true;
@@ -649,7 +680,7 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
     const int type = n->type & RT_TYPE_MASK;
     if (type == RT_NODE_BVH) {
       if constexpr ((F & F_COUNT) != 0) ++cnt.box;
-      if (box_hit(n->f, t.ray, t_min, t.closest, joint)) {
+      if (box_hit(n->f, t.ray, t_min, t.closest_up, joint)) {
         const int c = n->c;
         const bool flip = (c & RT_BVH_ORDERED) && comp(t.ray.d, c & 3) < 0;
         stk[(t.sp++) * stride] = flip ? n->a : n->b;
@@ -666,7 +697,8 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
 }
 
 // The closest hit's record, built once from the same ray with the same operations (a chain
-// hit is re-run under the bound that was in force when it was found).
+// hit is re-run under the bound that was in force when it was found). Callers check `tie`
+// first and re-walk with trav_restart_ref.
 template <unsigned F>
 __device__ __forceinline__ bool trav_finish(const Scene& S, const Trav& t, const Ray& r, double t_min, Hit& h) {
   if (t.best_node < 0) return false;
