@@ -186,7 +186,8 @@ def test_resumable_walks_closest_hits(gpu_ctx, name, walk):
         os.makedirs("gpurun_out", exist_ok=True)
         np.savez(f"gpurun_out/walk_{name}_{walk}.npz", rays=rays[bad], got=got[bad], ref=ref[bad])
     assert not bad.any(), f"{int(bad.sum())} of {len(rays)} rays differ"
-    assert np.all(np.abs(got[:, 8:10] - ref[:, 8:10]) <= 4e-16)
+    du = np.abs(got[:, 8:10] - ref[:, 8:10])  # sphere u, v: OCML vs glibc atan/asin ulps
+    assert np.all(du <= 2e-15), f"u/v max |d| {du.max():.3g}"
 
 
 @pytest.mark.parametrize("name,cam", [("random_book_one", "random_scene"), ("cornell", "cornell")])
@@ -197,6 +198,7 @@ def test_walks_output_identical(gpu_ctx, name, cam, monkeypatch):
     c = rtamd.camera(cam, 160, 96)
     gpu_ctx.upload(sc)
     p = rtamd.make_params(160, 96, 4, 50, rtamd.RT_RNG_PHILOX, seed=5)
+    monkeypatch.setenv("RTAMD_WIDE", "1")
     rgb_w, lin_w, _ = gpu_ctx.render(c, p, linear=True)
     monkeypatch.setenv("RTAMD_WIDE", "0")
     rgb_b, lin_b, _ = gpu_ctx.render(c, p, linear=True)
