@@ -329,8 +329,13 @@ struct WideBuilder {
     int child_need = 0;
     for (int k = 0; k < RT_WIDE; ++k) {
       if (k >= (int)kids.size()) {
+        // unused slot: an empty box (never accepted by a finite test) over a harmless leaf — the
+        // first leaf below this node, re-testing which cannot change the closest hit — so that
+        // rays accepting every child (fp32 slack = inf) need no slot check
         for (int a = 0; a < 3; ++a) { w.lo[a][k] = INFINITY; w.hi[a][k] = -INFINITY; }
-        w.child[k] = RT_WIDE_EMPTY;
+        int leaf = kids[0];
+        while (nodes[leaf].type == RT_NODE_BVH) leaf = nodes[leaf].a;
+        w.child[k] = ~leaf;
         continue;
       }
       Box b;

@@ -17,6 +17,9 @@
 #ifndef RT_STACK
 #define RT_STACK 32 /* traversal stack entries per lane (LDS) */
 #endif
+#ifndef RT_WSTACK
+#define RT_WSTACK 48 /* the same for the 4-wide walk (up to 3 siblings stacked per level) */
+#endif
 #define RT_LIGHT_DEPTH 2  /* max BVH depth of the lights tree (host-validated) */
 #define RT_FRAME 0x40000000 /* stack-entry tag: instance frame marker */
 #define RT_CHAIN_PRIM 0x100 /* device node type flag: Translate/Rotate chain ending in a primitive */

@@ -325,15 +325,29 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
   const bool joint = !(A.flags & RT_FLAG_REFERENCE_CULL);
 
   long long w = -1;
-  bool done = false, path = false, walking = false, ready = false;
+  bool done = false, walking = false, ready = false;
   int px = 0, row = 0, s = 0, depth = 0;
-  Ray ray;
   V3 thr = v3(0, 0, 0), sum = v3(0, 0, 0);
   RngPhilox g;
   g.init(A.seed, 0, 0);
-  Trav t;
-  Cnt cnt{0, 0, 0, 0};
+  Trav t;  // the segment's ray lives only here between segments (no second copy is carried)
+  Cnt cnt{0, 0, 0, 0, 0};
   unsigned long long segs = 0, blocks = 0, samples = 0, ph_setup = 0, ph_trav = 0, ph_shade = 0;
+
+  // sample s of pixel w is over: add its colour; the pixel is done after spp samples
+  auto end_sample = [&](V3 contrib) {
+    if constexpr ((F & F_COUNT) != 0) {
+      blocks += g.pair;
+      ++samples;
+    }
+    sum = sum + contrib;
+    ++s;
+    const bool all_nan = (A.flags & RT_FLAG_NAN_CULL) && sum.x != sum.x && sum.y != sum.y && sum.z != sum.z;
+    if (s == A.spp || all_nan) {
+      store_pixel(A, w, divide(sum, (double)A.spp));
+      w = -1;
+    }
+  };
 
   for (;;) {
     unsigned long long s0 = 0;
@@ -347,21 +361,17 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     if (ready) {
       ready = false;
       Hit h;
+      Ray ray = plain(t.ray);
       const bool got = trav_finish<F>(S, t, ray, kEps, h);
       V3 contrib;
       if (shade_hit<F>(S, got, h, ray, thr, depth, g, contrib, cnt)) {
-        if constexpr ((F & F_COUNT) != 0) {
-          blocks += g.pair;
-          ++samples;
-        }
-        sum = sum + contrib;
-        path = false;
-        ++s;
-        const bool all_nan = (A.flags & RT_FLAG_NAN_CULL) && sum.x != sum.x && sum.y != sum.y && sum.z != sum.z;
-        if (s == A.spp || all_nan) {
-          store_pixel(A, w, divide(sum, (double)A.spp));
-          w = -1;
-        }
+        end_sample(contrib);
+      } else if (depth <= 0) {  // rayColor's d <= 0 -> black (thr * 0 keeps a NaN throughput NaN)
+        end_sample(vmul(thr, v3(0.0, 0.0, 0.0)));
+      } else {  // next segment of the same path
+        trav_begin<F>(t, ray, S.world, kEps, INFINITY);
+        walking = true;
+        if constexpr ((F & F_COUNT) != 0) ++segs;
       }
     }
     unsigned long long s0b = 0;
@@ -384,36 +394,22 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
             w = wi;
             s = 0;
             sum = v3(0, 0, 0);
-            path = false;
           }
         }
       }
       if (w < 0) break;  // no work left for this lane
-      if (!path) {  // start sample s: uniformRandomUVs' pair, then getRay
-        const uint32_t pid = (uint32_t)((long long)row * A.W + px);
-        g.init(A.seed, pid, (uint32_t)s);
-        const double ru = g.draw(), rv = g.draw();
-        const int y = A.H - 1 - row;
-        const double u = ((double)px + ru) / (double)A.W;
-        const double v = ((double)y + rv) / (double)A.H;
-        ray = get_ray(A.cam, u, v, g);
-        thr = v3(1.0, 1.0, 1.0);
-        depth = A.max_depth;
-        path = true;
-      }
-      if (depth <= 0) {  // d <= 0 -> black; the sample ends without a walk
-        if constexpr ((F & F_COUNT) != 0) {
-          blocks += g.pair;
-          ++samples;
-        }
-        sum = sum + vmul(thr, v3(0.0, 0.0, 0.0));
-        path = false;
-        ++s;
-        const bool all_nan = (A.flags & RT_FLAG_NAN_CULL) && sum.x != sum.x && sum.y != sum.y && sum.z != sum.z;
-        if (s == A.spp || all_nan) {
-          store_pixel(A, w, divide(sum, (double)A.spp));
-          w = -1;
-        }
+      // start sample s: uniformRandomUVs' pair, then getRay
+      const uint32_t pid = (uint32_t)((long long)row * A.W + px);
+      g.init(A.seed, pid, (uint32_t)s);
+      const double ru = g.draw(), rv = g.draw();
+      const int y = A.H - 1 - row;
+      const double u = ((double)px + ru) / (double)A.W;
+      const double v = ((double)y + rv) / (double)A.H;
+      const Ray ray = get_ray(A.cam, u, v, g);
+      thr = v3(1.0, 1.0, 1.0);
+      depth = A.max_depth;
+      if (depth <= 0) {
+        end_sample(vmul(thr, v3(0.0, 0.0, 0.0)));
         continue;
       }
       trav_begin<F>(t, ray, S.world, kEps, INFINITY);
@@ -459,7 +455,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
 
 template <unsigned F, int WAVES>
 __global__ void __launch_bounds__(RT_BLOCK, WAVES) render_philox2(RenderArgs A) {
-  __shared__ int stk_mem[RT_STACK * RT_BLOCK];
+  __shared__ int stk_mem[((F & F_WIDE) ? RT_WSTACK : RT_STACK) * RT_BLOCK];
   philox_loop2<F>(A, A.S, &stk_mem[threadIdx.x], RT_BLOCK);
 }
 
@@ -548,7 +544,7 @@ __global__ void assemble(const T* slabs, T* image, int W, int H, int tile, int t
 template <unsigned F>
 __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* rays, int n, double tmin,
                                                          double tmax, uint64_t seed, int joint, int walk, double* out) {
-  __shared__ int stk_mem[RT_STACK * RT_BLOCK];
+  __shared__ int stk_mem[((F & F_WIDE) ? RT_WSTACK : RT_STACK) * RT_BLOCK];
   int* stk = &stk_mem[threadIdx.x];
   const int i = blockIdx.x * RT_BLOCK + threadIdx.x;
   if (i >= n) return;
@@ -943,7 +939,9 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   const bool want_wide = wenv ? wenv[0] != '0' : c->rebuilt_bvh;
   const bool wide = replace && c->d_wnodes && !(p->flags & RT_FLAG_REFERENCE_CULL) && want_wide;
   const int loop = wide ? 2 : (replace ? 1 : 0);
-  const int waves = var == kVarSpheres ? waves_target(3) : waves_target(1);
+  // waves per SIMD (measured, C2 / C3): spheres 3 (W=2: -11 %); Cornell 2 on the replacement
+  // loop (578 vs 409 Msamples/s at 1), 1 on the per-sample loop
+  const int waves = var == kVarSpheres ? waves_target(3) : waves_target(loop ? 2 : 1);
   // LDS-staged kernel when the traversal's node array plus the stacks fit one CU's 160 KiB
   // (RTAMD_LDS=0 disables it for A/B runs).
   if (!count && !env_off("RTAMD_LDS") && var != F_ALL) {
@@ -1112,7 +1110,7 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
   if (c->replace_ok) {  // 4-wide fp32-box tree over the same world tree (unflagged node copy)
     std::vector<rt_wnode> wide;
     int need = 0;
-    if (rt::build_wide_bvh(nodes, d->world_root, wide, &need) && need + 2 <= RT_STACK &&
+    if (rt::build_wide_bvh(nodes, d->world_root, wide, &need) && need + 2 <= RT_WSTACK &&
         (size_t)wide.size() < (size_t)INT32_MAX / 2) {
       if ((rc = upload(&c->d_wnodes, wide.data(), wide.size()))) {
         free_scene(c);

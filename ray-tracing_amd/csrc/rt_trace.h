@@ -500,9 +500,8 @@ struct Trav {
   bool ref;           // the reference's own walk: caller's tree, left first, bound = closest
   // F_WIDE: the ray in fp32 for the conservative child-box test (wide_children)
   float o32x, o32y, o32z, i32x, i32y, i32z;
-  float slack, tmin32, tmax32;
+  float slack, tmin32, tmax32;  // slack = +inf: the fp32 distances say nothing, accept every child
   unsigned oct;   // bit a: the ray runs towards -axis a (its near plane is the box's hi)
-  bool all;       // a direction component too small for fp32: accept every child
 };
 
 __device__ __forceinline__ float f32_lower(double x) {  // <= x (or -inf)
@@ -547,7 +546,7 @@ __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r, int root, doub
     const bool bad = (isinf(t.i32x) & (r.d.x != 0.0)) | (isinf(t.i32y) & (r.d.y != 0.0)) |
                      (isinf(t.i32z) & (r.d.z != 0.0)) | isnan(t.i32x) | isnan(t.i32y) | isnan(t.i32z) |
                      !isfinite(t.o32x) | !isfinite(t.o32y) | !isfinite(t.o32z) | isnan(t.slack);
-    t.all = bad;
+    if (bad) t.slack = INFINITY;  // accept every child (empty slots hold a harmless leaf)
   }
 }
 
@@ -581,7 +580,7 @@ __device__ __forceinline__ void trav_take(Trav& t, double x, int id, int sub) {
     t.best_node = id;
     t.best_sub = sub;
     if constexpr ((F & F_WIDE) != 0) t.tmax32 = f32_upper(x);
-  } else if (x == t.closest) {
+  } else if (x == t.closest && id != t.best_node) {  // (the same leaf twice is no tie)
     t.tie = true;
   }
 }
@@ -615,9 +614,11 @@ __device__ __forceinline__ float wide_key(const Trav& t, float nx, float ny, flo
   const float tfx = (fx - t.o32x) * t.i32x, tfy = (fy - t.o32y) * t.i32y, tfz = (fz - t.o32z) * t.i32z;
   const float near = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, t.tmin32));
   const float far = fminf(fminf(tfx, tfy), fminf(tfz, t.tmax32));
-  // (an infinite near or far — a parallel ray outside the slab — must not widen the margin)
+  // (an infinite near or far — a parallel ray outside the slab — must not widen the margin; a NaN
+  // difference, +inf - +inf, is accepted)
   const float mag = fminf(fmaxf(fabsf(near), fabsf(far)), 3.0e38f);
-  const bool hit = ((near - far <= fmaf(mag, 0x1p-20f, t.slack)) | t.all) & (child != RT_WIDE_EMPTY);
+  const bool hit = !(near - far > fmaf(mag, 0x1p-20f, t.slack));
+  (void)child;
   return hit ? fminf(near, 3.0e38f) : INFINITY;
 }
 
@@ -702,7 +703,8 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
 template <unsigned F>
 __device__ __forceinline__ bool trav_finish(const Scene& S, const Trav& t, const Ray& r, double t_min, Hit& h) {
   if (t.best_node < 0) return false;
-  if (t.best_sub < 0) return chain_hit<F>(S, t.best_node, r, t_min, t.best_tmax, h);
+  if constexpr ((F & F_INST) != 0)
+    if (t.best_sub < 0) return chain_hit<F>(S, t.best_node, r, t_min, t.best_tmax, h);
   prim_record<F>(S, &S.nodes[t.best_node], t.best_sub, r, t.closest, h);
   return true;
 }

@@ -6,17 +6,17 @@
 // (lo[axis][child], hi[axis][child]), rounded OUTWARD from the fp64 boxes so that each box
 // contains the double-precision one, then four child references. The fp32 test over these boxes
 // only culls (it accepts every ray the fp64 slab test over the same boxes accepts, see
-// wide_children in rt_trace.h); every leaf is still hit-tested in fp64 exactly as the reference.
+// wide_key in rt_trace.h); every leaf is still hit-tested in fp64 exactly as the reference.
 #pragma once
 #include <stdint.h>
 
 #define RT_WIDE 4
-#define RT_WIDE_EMPTY ((int32_t)0x80000000)  // unused child slot (its box is empty: lo = +inf, hi = -inf)
 
 typedef struct rt_wnode {
   float lo[3][RT_WIDE];
   float hi[3][RT_WIDE];
-  int32_t child[RT_WIDE];  // >= 0: wide node id; < 0: leaf, ~child = flat rt_node id; RT_WIDE_EMPTY
+  int32_t child[RT_WIDE];  // >= 0: wide node id; < 0: leaf, ~child = flat rt_node id (an unused
+                           // slot: empty box lo = +inf, hi = -inf over a leaf of this node)
   int32_t pad[RT_WIDE];
 } rt_wnode;
 

@@ -187,6 +187,7 @@ def test_resumable_walks_closest_hits(gpu_ctx, name, walk):
         np.savez(f"gpurun_out/walk_{name}_{walk}.npz", rays=rays[bad], got=got[bad], ref=ref[bad])
     assert not bad.any(), f"{int(bad.sum())} of {len(rays)} rays differ"
     du = np.abs(got[:, 8:10] - ref[:, 8:10])  # sphere u, v: OCML vs glibc atan/asin ulps
+    du[np.isnan(got[:, 8:10]) & np.isnan(ref[:, 8:10])] = 0  # asin of |y| > 1 by rounding: NaN in both
     assert np.all(du <= 2e-15), f"u/v max |d| {du.max():.3g}"
 
 
