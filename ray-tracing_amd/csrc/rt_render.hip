@@ -335,7 +335,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
   unsigned long long segs = 0, blocks = 0, samples = 0, ph_setup = 0, ph_trav = 0, ph_shade = 0;
 
   // sample s of pixel w is over: add its colour; the pixel is done after spp samples
-  auto end_sample = [&](V3 contrib) {
+  auto end_sample = [&](V3 contrib) __attribute__((always_inline)) {
     if constexpr ((F & F_COUNT) != 0) {
       blocks += g.pair;
       ++samples;

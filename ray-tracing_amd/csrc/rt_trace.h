@@ -498,7 +498,7 @@ struct Trav {
   int node, sp, best_node, best_sub;
   bool tie;           // a second leaf hit at exactly `closest`: the walk is redone with `ref`
   bool ref;           // the reference's own walk: caller's tree, left first, bound = closest
-  // F_WIDE: the ray in fp32 for the conservative child-box test (wide_children)
+  // F_WIDE: the ray in fp32 for the conservative child-box test (wide_keys2)
   float o32x, o32y, o32z, i32x, i32y, i32z;
   float slack, tmin32, tmax32;  // slack = +inf: the fp32 distances say nothing, accept every child
   unsigned oct;   // bit a: the ray runs towards -axis a (its near plane is the box's hi)
@@ -541,12 +541,20 @@ __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r, int root, doub
     t.tmin32 = f32_lower(t_min);
     t.tmax32 = f32_upper(t_max);
     t.oct = (signbit(t.i32x) ? 1u : 0u) | (signbit(t.i32y) ? 2u : 0u) | (signbit(t.i32z) ? 4u : 0u);
-    // 1/d overflowing fp32 for d != 0 (|d| < 2^-126), a NaN direction or a non-finite origin:
-    // the fp32 distances say nothing, every child is entered (the leaves still decide exactly)
+    // 1/d overflowing fp32 for d != 0 (|d| < 2^-126), a NaN direction, a non-finite origin, or
+    // t_min <= 0 (wide_key's scaling needs near > 0): the fp32 distances say nothing. All plane
+    // distances become 0 and the slack infinite, so every child is entered (leaves decide).
     const bool bad = (isinf(t.i32x) & (r.d.x != 0.0)) | (isinf(t.i32y) & (r.d.y != 0.0)) |
                      (isinf(t.i32z) & (r.d.z != 0.0)) | isnan(t.i32x) | isnan(t.i32y) | isnan(t.i32z) |
-                     !isfinite(t.o32x) | !isfinite(t.o32y) | !isfinite(t.o32z) | isnan(t.slack);
-    if (bad) t.slack = INFINITY;  // accept every child (empty slots hold a harmless leaf)
+                     !isfinite(t.o32x) | !isfinite(t.o32y) | !isfinite(t.o32z) | isnan(t.slack) |
+                     !(t.tmin32 > 0.0f);
+    t.o32x = bad ? 0.0f : t.o32x;
+    t.o32y = bad ? 0.0f : t.o32y;
+    t.o32z = bad ? 0.0f : t.o32z;
+    t.i32x = bad ? 0.0f : t.i32x;
+    t.i32y = bad ? 0.0f : t.i32y;
+    t.i32z = bad ? 0.0f : t.i32z;
+    t.slack = bad ? INFINITY : t.slack;
   }
 }
 
@@ -600,26 +608,32 @@ __device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, int id, doubl
   }
 }
 
-// Conservative fp32 slab test of one child box (the rows hold the near / far planes per axis).
-// Each plane distance (plane - o32) * i32 is within eps*(K + 3|t|) of the exact distance to the
-// fp32 box (eps = 2^-24, K = max |o * (1/d)| over finite axes); the test accepts when
-// near - far <= 2^-20 * (max(|near|, |far|) + K), so it accepts every ray whose exact slab interval
-// over the box is non-empty, and the fp32 box contains the fp64 one. A zero direction component
-// gives i32 = +-inf: its distances are +-inf (origin outside the slab: the ray misses, or the
-// axis does not constrain), or NaN exactly when the origin lies on the plane, which fmaxf/fminf
-// (IEEE maxNum/minNum) drop — the plane then does not constrain, as for a ray inside the slab.
-__device__ __forceinline__ float wide_key(const Trav& t, float nx, float ny, float nz, float fx, float fy, float fz,
-                                          int child) {
-  const float tnx = (nx - t.o32x) * t.i32x, tny = (ny - t.o32y) * t.i32y, tnz = (nz - t.o32z) * t.i32z;
-  const float tfx = (fx - t.o32x) * t.i32x, tfy = (fy - t.o32y) * t.i32y, tfz = (fz - t.o32z) * t.i32z;
-  const float near = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, t.tmin32));
-  const float far = fminf(fminf(tfx, tfy), fminf(tfz, t.tmax32));
-  // (an infinite near or far — a parallel ray outside the slab — must not widen the margin; a NaN
-  // difference, +inf - +inf, is accepted)
-  const float mag = fminf(fmaxf(fabsf(near), fabsf(far)), 3.0e38f);
-  const bool hit = !(near - far > fmaf(mag, 0x1p-20f, t.slack));
-  (void)child;
-  return hit ? fminf(near, 3.0e38f) : INFINITY;
+// Conservative fp32 slab test of the child boxes (two at a time in packed fp32). Each plane
+// distance (plane - o32) * i32 is within eps*(K + 3|t|) of the exact distance to the fp32 box
+// (eps = 2^-24, K = max |o * (1/d)| over finite axes; the fp32 box contains the fp64 one). With
+// near >= tmin > 0, the test near*(1 - 2^-21) <= far*(1 + 2^-21) + 2^-20*K accepts every ray
+// whose exact slab interval over the box meets [tmin, tmax]: for far >= 0 the relative margin
+// covers 3eps(|near| + |far|) and the slack 2eps*K; a computed far < 0 with an exact far >= tmin
+// means far <= eps*K, which the slack covers. A zero direction component gives i32 = +-inf: its
+// distances are +-inf (origin outside the slab: near = +inf or far = -inf, rejected; inside:
+// no constraint), or NaN exactly when the origin lies on the plane, which fmaxf/fminf (IEEE
+// maxNum/minNum) drop — the plane then does not constrain, as for a ray inside the slab.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void wide_keys2(const Trav& t, f32x2 nx, f32x2 ny, f32x2 nz, f32x2 fx, f32x2 fy, f32x2 fz,
+                                           float& k0, float& k1) {
+  const f32x2 ox = {t.o32x, t.o32x}, oy = {t.o32y, t.o32y}, oz = {t.o32z, t.o32z};
+  const f32x2 ix = {t.i32x, t.i32x}, iy = {t.i32y, t.i32y}, iz = {t.i32z, t.i32z};
+  const f32x2 tnx = (nx - ox) * ix, tny = (ny - oy) * iy, tnz = (nz - oz) * iz;
+  const f32x2 tfx = (fx - ox) * ix, tfy = (fy - oy) * iy, tfz = (fz - oz) * iz;
+  const float n0 = fmaxf(fmaxf(tnx.x, tny.x), fmaxf(tnz.x, t.tmin32));
+  const float n1 = fmaxf(fmaxf(tnx.y, tny.y), fmaxf(tnz.y, t.tmin32));
+  const float f0 = fminf(fminf(tfx.x, tfy.x), fminf(tfz.x, t.tmax32));
+  const float f1 = fminf(fminf(tfx.y, tfy.y), fminf(tfz.y, t.tmax32));
+  const bool h0 = n0 * (1.0f - 0x1p-21f) <= fmaf(f0, 1.0f + 0x1p-21f, t.slack);
+  const bool h1 = n1 * (1.0f - 0x1p-21f) <= fmaf(f1, 1.0f + 0x1p-21f, t.slack);
+  k0 = h0 ? fminf(n0, 3.0e38f) : INFINITY;
+  k1 = h1 ? fminf(n1, 3.0e38f) : INFINITY;
 }
 
 __device__ __forceinline__ void cswap(float& ka, int& ca, float& kb, int& cb) {
@@ -644,10 +658,11 @@ __device__ __forceinline__ bool wide_node(const Scene& S, Trav& t, int* stk, int
   const float4 fy = *reinterpret_cast<const float4*>(base + (oy < 12 ? oy + 12 : oy - 12));
   const float4 fz = *reinterpret_cast<const float4*>(base + (oz < 12 ? oz + 12 : oz - 12));
   const int4 ch = *reinterpret_cast<const int4*>(base + 24);
-  float k0 = wide_key(t, nx.x, ny.x, nz.x, fx.x, fy.x, fz.x, ch.x);
-  float k1 = wide_key(t, nx.y, ny.y, nz.y, fx.y, fy.y, fz.y, ch.y);
-  float k2 = wide_key(t, nx.z, ny.z, nz.z, fx.z, fy.z, fz.z, ch.z);
-  float k3 = wide_key(t, nx.w, ny.w, nz.w, fx.w, fy.w, fz.w, ch.w);
+  float k0, k1, k2, k3;
+  wide_keys2(t, f32x2{nx.x, nx.y}, f32x2{ny.x, ny.y}, f32x2{nz.x, nz.y}, f32x2{fx.x, fx.y}, f32x2{fy.x, fy.y},
+             f32x2{fz.x, fz.y}, k0, k1);
+  wide_keys2(t, f32x2{nx.z, nx.w}, f32x2{ny.z, ny.w}, f32x2{nz.z, nz.w}, f32x2{fx.z, fx.w}, f32x2{fy.z, fy.w},
+             f32x2{fz.z, fz.w}, k2, k3);
   int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
   const int n_hit = (k0 < INFINITY) + (k1 < INFINITY) + (k2 < INFINITY) + (k3 < INFINITY);
   cswap(k0, c0, k1, c1);

@@ -6,7 +6,7 @@
 // (lo[axis][child], hi[axis][child]), rounded OUTWARD from the fp64 boxes so that each box
 // contains the double-precision one, then four child references. The fp32 test over these boxes
 // only culls (it accepts every ray the fp64 slab test over the same boxes accepts, see
-// wide_key in rt_trace.h); every leaf is still hit-tested in fp64 exactly as the reference.
+// wide_keys2 in rt_trace.h); every leaf is still hit-tested in fp64 exactly as the reference.
 #pragma once
 #include <stdint.h>
 
