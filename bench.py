@@ -39,15 +39,19 @@ CONFIGS = {
 # MI355X peaks (MI355X_MICROARCH.md chip table; FP64 vector = half the FP32 vector peak).
 HBM_PEAK_GBS = 8000.0
 FP64_PEAK_TFLOPS = 78.6
+FP32_PEAK_TFLOPS = 157.3
 
 # Algorithmic bytes per unit of device-counted work (DESIGN.md "Roofline"): every BVH box test,
 # leaf test and instance/medium test reads one 64-byte rt_node; every traced segment reads its
 # hit material + texture (24 + 48 B); every light-pdf evaluation reads the light record (64 B);
 # every pixel writes 3 bytes.
-BYTES = {"box_tests": 64, "prim_tests": 64, "other_tests": 64, "segments": 72, "light_pdfs": 64}
+BYTES = {"box_tests": 64, "prim_tests": 64, "other_tests": 64, "segments": 72, "light_pdfs": 64,
+         "wide_nodes": 128}  # a 4-wide node: four fp32 child boxes + four child ids (rt_wide.h)
 # fp64 operations per unit (lower bound): box test 6 sub + 6 div + 6 min/max,
 # sphere test ~30, scatter/shading ~60 per segment.
 FLOPS = {"box_tests": 18, "prim_tests": 30, "other_tests": 30, "segments": 60}
+# fp32 operations per 4-wide node: 4 children x (6 sub + 6 mul + 6 min/max + 3 for the test)
+FLOPS32 = {"wide_nodes": 84}
 
 
 def log(*a):
@@ -262,6 +266,10 @@ def main():
                                        "build of the same launch; the binding roof is FP64 VALU (see fp64)"}
             out["fp64"] = {"achieved_tflops": round(fl, 3), "peak_tflops": FP64_PEAK_TFLOPS,
                            "frac": round(fl / FP64_PEAK_TFLOPS, 5), "flops_per_sample": round(flops_per_sample, 1)}
+            f32 = sum(FLOPS32[k] * per.get(k, 0) for k in FLOPS32)
+            fl32 = f32 * samples_per_launch / (kernel_avg * 1e-3) / 1e12
+            out["fp32"] = {"achieved_tflops": round(fl32, 3), "peak_tflops": FP32_PEAK_TFLOPS,
+                           "frac": round(fl32 / FP32_PEAK_TFLOPS, 5), "flops_per_sample": round(f32, 1)}
             out["work_per_sample"] = {k: round(v, 3) for k, v in per.items() if k != "samples"}
             if counters:
                 out["work_per_sample_reference_cull"] = {k: round(v / max(1, counters["samples"]), 3)
