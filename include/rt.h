@@ -299,6 +299,11 @@ int rt_upload_scene_ex(rt_ctx* ctx, const rt_scene_desc* desc, uint32_t flags);
 /* The rebuild rt_upload_scene applies, on the host: the node array with the new world BVH
  * appended (out_nodes NULL: size query) and the new world root (== the old one if ineligible). */
 int rt_rebuild_bvh(const rt_scene_desc* desc, rt_node* out_nodes, int capacity, int* out_n, int* out_root);
+/* The 4-wide collapse the device walk uses (rt_wide.h records, 128 B each) of the binary tree at
+ * `root` of a node array (e.g. rt_rebuild_bvh's output): out NULL = size query. out_stack_need
+ * = the walk's stack bound (entries). RT_E_UNSUPPORTED when the root is not a BVH node. */
+int rt_wide_bvh(const rt_node* nodes, int n_nodes, int root, void* out, int capacity, int* out_n,
+                int* out_stack_need);
 
 /*
  * Blocking full-image render (replaces runRender, src/Lib.hs:1491).

@@ -395,3 +395,28 @@ extern "C" int rt_rebuild_bvh(const rt_scene_desc* in, rt_node* out_nodes, int c
   }
   return RT_OK;
 }
+
+extern "C" int rt_wide_bvh(const rt_node* nodes, int n_nodes, int root, void* out, int capacity, int* out_n,
+                           int* out_stack_need) {
+  if (!nodes || n_nodes <= 0 || root < 0 || root >= n_nodes || !out_n || !out_stack_need) {
+    rt::set_error("rt_wide_bvh: bad argument");
+    return RT_E_INVALID;
+  }
+  std::vector<rt_node> v(nodes, nodes + n_nodes);
+  std::vector<rt_wnode> w;
+  int need = 0;
+  if (!rt::build_wide_bvh(v, root, w, &need)) {
+    rt::set_error("rt_wide_bvh: the root is not a BVH node (or a box is not boundable)");
+    return RT_E_UNSUPPORTED;
+  }
+  *out_n = (int)w.size();
+  *out_stack_need = need;
+  if (out) {
+    if (capacity < (int)w.size()) {
+      rt::set_error("rt_wide_bvh: capacity too small");
+      return RT_E_INVALID;
+    }
+    std::copy(w.begin(), w.end(), static_cast<rt_wnode*>(out));
+  }
+  return RT_OK;
+}

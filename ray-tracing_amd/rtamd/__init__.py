@@ -107,7 +107,11 @@ EXPORTED = [
     "rt_device_count", "rt_create", "rt_destroy", "rt_upload_scene", "rt_render", "rt_shard_geometry",
     "rt_render_shard_async", "rt_assemble_async", "rt_assemble_linear_async", "rt_last_kernel_ms",
     "rt_debug_closest_hits", "rt_debug_math", "rt_render_work", "rt_upload_scene_ex", "rt_rebuild_bvh",
+    "rt_wide_bvh",
 ]
+
+# include/rt_wide.h: one 4-wide node (128 B)
+WNODE_DTYPE = np.dtype([("lo", "<f4", (3, 4)), ("hi", "<f4", (3, 4)), ("child", "<i4", (4,)), ("pad", "<i4", (4,))])
 
 _lib = None
 
@@ -162,6 +166,7 @@ def lib() -> C.CDLL:
             "rt_render_work": (I, [C.c_void_p, P(rt_camera), P(rt_render_params), P(U64)]),
             "rt_upload_scene_ex": (I, [C.c_void_p, P(rt_scene_desc), C.c_uint32]),
             "rt_rebuild_bvh": (I, [P(rt_scene_desc), P(rt_node), I, P(I), P(I)]),
+            "rt_wide_bvh": (I, [P(rt_node), I, I, C.c_void_p, I, P(I), P(I)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -335,6 +340,19 @@ def rebuilt_scene(scene: Scene) -> Scene:
     s = Scene(scene._builder, d)
     s._keep = (arr, scene)
     return s
+
+
+def wide_bvh(scene: Scene, root: Optional[int] = None) -> Tuple[np.ndarray, int]:
+    """rt_wide_bvh: the 4-wide collapse of the binary tree at `root` (default: the scene's world
+    root) as WNODE_DTYPE records, and the walk's stack bound."""
+    n, need = C.c_int(0), C.c_int(0)
+    r = scene.desc.world_root if root is None else root
+    _check(lib().rt_wide_bvh(scene.desc.nodes, scene.desc.n_nodes, r, None, 0, C.byref(n), C.byref(need)),
+           "rt_wide_bvh")
+    out = np.zeros(n.value, dtype=WNODE_DTYPE)
+    _check(lib().rt_wide_bvh(scene.desc.nodes, scene.desc.n_nodes, r, out.ctypes.data_as(C.c_void_p), n.value,
+                             C.byref(n), C.byref(need)), "rt_wide_bvh")
+    return out, need.value
 
 
 def make_scene(name: str, gen: Tuple[int, int], t0: float = 0.0, t1: float = 1.0,
