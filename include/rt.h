@@ -171,10 +171,19 @@ typedef struct rt_camera {
  *  RT_RNG_PHILOX (tier B): one Philox4x32-10 stream per (pixel, sample), key = seed,
  *                counter = {draw_pair, sample, pixel_id, 0}; each 128-bit block yields two
  *                64-bit words, converted exactly as random-1.2.0 `random :: Double`.
- *                Samples are summed in sample order. Embarrassingly parallel.
+ *                A pixel's samples are summed in fixed chunks: chunk k holds samples
+ *                [k*CH, min(spp, (k+1)*CH)) with CH = rt_sample_chunk(spp); each chunk is
+ *                summed in sample order from 0, the chunk sums in chunk order from 0. (The
+ *                chunks are the device's work-items; a fixed definition keeps the image
+ *                independent of scheduling and shard count.) Embarrassingly parallel.
  */
 #define RT_RNG_EXACT 0
 #define RT_RNG_PHILOX 1
+#define RT_SAMPLE_CHUNKS 32 /* at most this many chunks per pixel */
+static inline int rt_sample_chunk(int spp) {
+  const int k = spp < RT_SAMPLE_CHUNKS ? spp : RT_SAMPLE_CHUNKS;
+  return k > 0 ? (spp + k - 1) / k : 1;
+}
 
 /* Flags. */
 #define RT_FLAG_NAN_CULL 1u /* tier B only: stop tracing a pixel once its sum is NaN

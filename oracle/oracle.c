@@ -665,25 +665,32 @@ static V3 render_pixel_exact(const Ctx* c, int x, int y, Rng* g, double* uvbuf) 
     return divide(acc, (double)ns);
 }
 
-/* One pixel, tier B: sample s draws from its own Philox stream; summed in sample order. */
+/* One pixel, tier B: sample s draws from its own Philox stream; samples summed in sample order
+   within fixed chunks, chunk sums in chunk order (include/rt.h, rt_sample_chunk). */
 static V3 render_pixel_philox(const Ctx* c, int x, int y, uint32_t pid, uint64_t seed, int64_t* draws) {
     V3 acc = v3(0, 0, 0);
-    for (int s = 0; s < c->spp; ++s) {
-        Rng g;
-        memset(&g, 0, sizeof g);
-        g.mode = RT_RNG_PHILOX;
-        g.key[0] = (uint32_t)seed;
-        g.key[1] = (uint32_t)(seed >> 32);
-        g.sample = (uint32_t)s;
-        g.pid = pid;
-        g.draws = draws;
-        double ru = D(&g), rv = D(&g);
-        double u = ((double)x + ru) / (double)c->width;
-        double v = ((double)y + rv) / (double)c->height;
-        Ray r = get_ray(c, u, v, &g);
-        V3 c1 = ray_color(c, r, c->max_depth, &g);
-        acc = vadd(acc, c1);
-        CNT(c, C_SAMPLES);
+    const int ch = rt_sample_chunk(c->spp);
+    for (int k0 = 0; k0 < c->spp; k0 += ch) {
+        V3 part = v3(0, 0, 0);
+        const int k1 = k0 + ch < c->spp ? k0 + ch : c->spp;
+        for (int s = k0; s < k1; ++s) {
+            Rng g;
+            memset(&g, 0, sizeof g);
+            g.mode = RT_RNG_PHILOX;
+            g.key[0] = (uint32_t)seed;
+            g.key[1] = (uint32_t)(seed >> 32);
+            g.sample = (uint32_t)s;
+            g.pid = pid;
+            g.draws = draws;
+            double ru = D(&g), rv = D(&g);
+            double u = ((double)x + ru) / (double)c->width;
+            double v = ((double)y + rv) / (double)c->height;
+            Ray r = get_ray(c, u, v, &g);
+            V3 c1 = ray_color(c, r, c->max_depth, &g);
+            part = vadd(part, c1);
+            CNT(c, C_SAMPLES);
+        }
+        acc = vadd(acc, part);
     }
     return divide(acc, (double)c->spp);
 }

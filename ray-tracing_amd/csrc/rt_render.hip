@@ -53,7 +53,10 @@ struct RenderArgs {
   int W, H, spp, max_depth;
   uint32_t flags;
   int tile, tiles_x, tiles_total, shard_rank, shard_count;
-  long long work_total;  // slab pixels of this shard
+  long long work_total;  // work-items of this shard: slab pixels x sample chunks
+  long long slab;        // slab pixels of this shard
+  int chunk, chunks;     // tier B: samples per chunk (rt_sample_chunk) and chunks per pixel
+  double* partial;       // tier B: chunk sums, [chunk][slab pixel][3]
   uint64_t seed;
   unsigned long long* counter;
   unsigned long long* work;  // counting build: [segments, box, prim, other, light, blocks, samples]
@@ -63,7 +66,7 @@ struct RenderArgs {
   uint64_t* gens;  // tier A: per-column (seed, gamma), updated in place
 };
 
-// Slab work index -> image pixel (tile-major, 8x8 blocks inside a tile).
+// Slab pixel index -> image pixel (tile-major, 8x8 blocks inside a tile).
 __device__ __forceinline__ bool work_pixel(const RenderArgs& A, long long w, int& px, int& row) {
   const long long tp = (long long)A.tile * A.tile;
   const long long lt = w / tp;
@@ -76,6 +79,31 @@ __device__ __forceinline__ bool work_pixel(const RenderArgs& A, long long w, int
   px = tx * A.tile + (blk % bpr) * 8 + (l & 7);
   row = ty * A.tile + (blk / bpr) * 8 + (l >> 3);
   return px < A.W && row < A.H;
+}
+
+// Tier-B work-item -> (slab pixel, sample chunk). Items run tile by tile, chunk by chunk inside a
+// tile, so a wave's 64 consecutive items are one 8x8 pixel block at one chunk (coherent rays).
+// Returns false for pixels outside the image; else the sample range [s0, s1) and the chunk
+// sum's slot in `partial`.
+__device__ __forceinline__ bool work_item(const RenderArgs& A, long long wi, int& px, int& row, int& s0, int& s1,
+                                          long long& slot) {
+  const long long tp = (long long)A.tile * A.tile;
+  const long long per_tile = tp * A.chunks;
+  const long long lt = wi / per_tile;
+  const long long rem = wi - lt * per_tile;
+  const int k = (int)(rem / tp);
+  const long long idx = lt * tp + (rem - (long long)k * tp);
+  if (!work_pixel(A, idx, px, row)) return false;
+  s0 = k * A.chunk;
+  s1 = min(A.spp, s0 + A.chunk);
+  slot = (long long)k * A.slab + idx;
+  return s0 < s1;
+}
+__device__ __forceinline__ void store_partial(const RenderArgs& A, long long slot, V3 sum) {
+  double* q = A.partial + slot * 3;
+  q[0] = sum.x;
+  q[1] = sum.y;
+  q[2] = sum.z;
 }
 
 // getRay (Lib.hs:1253-1267): the disk and time draws always happen.
@@ -194,9 +222,9 @@ __device__ __forceinline__ void philox_loop(const RenderArgs& A, const Scene& S,
   const int lane = threadIdx.x & 63;
   const unsigned long long lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
-  long long w = -1;
+  long long w = -1;  // the current chunk's slot in A.partial
   bool done = false, path = false;
-  int px = 0, row = 0, s = 0, depth = 0;
+  int px = 0, row = 0, s = 0, s_end = 0, depth = 0;
   Ray ray;
   V3 thr = v3(0, 0, 0), sum = v3(0, 0, 0);
   RngPhilox g;
@@ -220,11 +248,11 @@ __device__ __forceinline__ void philox_loop(const RenderArgs& A, const Scene& S,
         const long long wi = (long long)(base + __popcll(mask & lanes_below));
         if (wi >= A.work_total) {
           done = true;
-        } else if (work_pixel(A, wi, px, row)) {
-          w = wi;
-          s = 0;
+        } else if (work_item(A, wi, px, row, s, s_end, w)) {
           sum = v3(0, 0, 0);
           path = false;
+        } else {
+          w = -1;
         }
       }
     }
@@ -263,8 +291,8 @@ __device__ __forceinline__ void philox_loop(const RenderArgs& A, const Scene& S,
       path = false;
       ++s;
       const bool all_nan = (A.flags & RT_FLAG_NAN_CULL) && sum.x != sum.x && sum.y != sum.y && sum.z != sum.z;
-      if (s == A.spp || all_nan) {
-        store_pixel(A, w, divide(sum, (double)A.spp));
+      if (s == s_end || all_nan) {
+        store_partial(A, w, sum);
         w = -1;
       }
     }
@@ -324,9 +352,9 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
   const unsigned long long lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const bool joint = !(A.flags & RT_FLAG_REFERENCE_CULL);
 
-  long long w = -1;
+  long long w = -1;  // the current chunk's slot in A.partial
   bool done = false, walking = false, ready = false;
-  int px = 0, row = 0, s = 0, depth = 0;
+  int px = 0, row = 0, s = 0, s_end = 0, depth = 0;
   V3 thr = v3(0, 0, 0), sum = v3(0, 0, 0);
   RngPhilox g;
   g.init(A.seed, 0, 0);
@@ -334,7 +362,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
   Cnt cnt{0, 0, 0, 0, 0};
   unsigned long long segs = 0, blocks = 0, samples = 0, ph_setup = 0, ph_trav = 0, ph_shade = 0;
 
-  // sample s of pixel w is over: add its colour; the pixel is done after spp samples
+  // sample s is over: add its colour; the chunk is done after its last sample
   auto end_sample = [&](V3 contrib) __attribute__((always_inline)) {
     if constexpr ((F & F_COUNT) != 0) {
       blocks += g.pair;
@@ -343,8 +371,8 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     sum = sum + contrib;
     ++s;
     const bool all_nan = (A.flags & RT_FLAG_NAN_CULL) && sum.x != sum.x && sum.y != sum.y && sum.z != sum.z;
-    if (s == A.spp || all_nan) {
-      store_pixel(A, w, divide(sum, (double)A.spp));
+    if (s == s_end || all_nan) {
+      store_partial(A, w, sum);
       w = -1;
     }
   };
@@ -390,10 +418,10 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
           const long long wi = (long long)(base + __popcll(mask & lanes_below));
           if (wi >= A.work_total) {
             done = true;
-          } else if (work_pixel(A, wi, px, row)) {
-            w = wi;
-            s = 0;
+          } else if (work_item(A, wi, px, row, s, s_end, w)) {
             sum = v3(0, 0, 0);
+          } else {
+            w = -1;
           }
         }
       }
@@ -480,6 +508,20 @@ __global__ void __launch_bounds__(WAVES * 256, WAVES) render_philox2_lds(RenderA
   int* stk = reinterpret_cast<int*>(lds + (size_t)n_nodes * rec) + threadIdx.x;
   (void)stack_entries;
   philox_loop2<F>(A, S, stk, WAVES * 256);
+}
+
+// Tier B: a slab pixel's chunk sums added in chunk order, then averaged and stored (rt.h).
+__global__ void __launch_bounds__(256) combine_chunks(RenderArgs A) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= A.slab) return;
+  int px, row;
+  if (!work_pixel(A, idx, px, row)) return;  // outside the image: never assembled
+  V3 acc = v3(0, 0, 0);
+  for (int k = 0; k < A.chunks; ++k) {
+    const double* q = A.partial + ((long long)k * A.slab + idx) * 3;
+    acc = acc + v3(q[0], q[1], q[2]);
+  }
+  store_pixel(A, idx, divide(acc, (double)A.spp));
 }
 
 // ---------------------------------------------------------------- tier A: the reference's stream
@@ -629,6 +671,8 @@ struct rt_ctx {
   bool replace_ok = false;  // media-free and no instance frames: the replacement loop applies
   bool has_scene = false;
   unsigned long long* d_counter = nullptr;
+  double* d_partial = nullptr;  // tier-B chunk sums (grown on demand)
+  size_t partial_bytes = 0;
   double last_ms = 0.0;
 };
 
@@ -903,6 +947,15 @@ unsigned scene_features(const rt_scene_desc* d) {
   return f;
 }
 
+int launch_combine(const RenderArgs& A, hipStream_t st) {
+  RenderArgs B = A;
+  void* args[] = {&B};
+  HIPCHK(hipLaunchKernel((const void*)combine_chunks, dim3((unsigned)((A.slab + 255) / 256)), dim3(256), args, 0,
+                         st));
+  HIPCHK(hipGetLastError());
+  return RT_OK;
+}
+
 int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int rank, int shards, uint8_t* d_rgb,
                   double* d_lin, hipStream_t st, unsigned long long* d_work = nullptr) {
   RenderArgs A{};
@@ -918,12 +971,27 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   A.tiles_total = (int)tiles_total;
   A.shard_rank = rank;
   A.shard_count = shards;
-  A.work_total = slab;
+  A.slab = slab;
+  A.chunk = rt_sample_chunk(p->spp);
+  A.chunks = (p->spp + A.chunk - 1) / A.chunk;
+  A.work_total = slab * A.chunks;
   A.seed = p->seed;
   A.counter = c->d_counter;
   A.work = d_work;
   A.out_rgb = d_rgb;
   A.out_lin = d_lin;
+  {  // chunk sums: [chunk][slab pixel][3] doubles, kept on the ctx and grown on demand
+    const size_t need = (size_t)A.chunks * (size_t)slab * 3 * sizeof(double);
+    if (need > c->partial_bytes) {
+      HIPCHK(hipStreamSynchronize(st));
+      (void)hipFree(c->d_partial);
+      c->d_partial = nullptr;
+      c->partial_bytes = 0;
+      HIPCHK(hipMalloc((void**)&c->d_partial, need));
+      c->partial_bytes = need;
+    }
+    A.partial = c->d_partial;
+  }
   HIPCHK(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned long long), st));
   const char* stop_env = std::getenv("RTAMD_TRAV_STOP");
   // refill when at most trav_stop/64 of a wave's live lanes still walk (measured: C2 flat at 2-8,
@@ -960,13 +1028,13 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
       HIPCHK(hipEventRecord(c->ev0, st));
       HIPCHK(hipLaunchKernel(fn, dim3(c->cu_count), dim3(block), args, bytes, st));
       HIPCHK(hipEventRecord(c->ev1, st));
-      return RT_OK;
+      return launch_combine(A, st);
     }
   }
   const void* fn = philox_kernel(var, loop, false, count ? 1 : waves, count);
   int bpc = 1;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, RT_BLOCK, 0));
-  const long long want = (slab + RT_BLOCK - 1) / RT_BLOCK;
+  const long long want = (A.work_total + RT_BLOCK - 1) / RT_BLOCK;
   const long long resident = (long long)c->cu_count * std::max(1, bpc);
   const int grid = (int)std::max(1ll, std::min(want, resident));
   HIPCHK(hipEventRecord(c->ev0, st));
@@ -974,7 +1042,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   HIPCHK(hipLaunchKernel(fn, dim3(grid), dim3(RT_BLOCK), args, 0, st));
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev1, st));
-  return RT_OK;
+  return launch_combine(A, st);
 }
 
 }  // namespace
@@ -1014,6 +1082,7 @@ void rt_destroy(rt_ctx* c) {
   (void)hipSetDevice(c->device);
   free_scene(c);
   (void)hipFree(c->d_counter);
+  (void)hipFree(c->d_partial);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
