@@ -61,6 +61,7 @@ struct RenderArgs {
   unsigned long long* counter;
   unsigned long long* work;  // counting build: [segments, box, prim, other, light, blocks, samples]
   int trav_stop;             // replacement loop: keep stepping while > trav_stop/64 of live lanes walk
+  int leaf_stop;             // 4-wide walk: leaf step once <= leaf_stop/64 of live lanes seek a leaf
   uint8_t* out_rgb;  // tier B: slab; tier A: image
   double* out_lin;
   uint64_t* gens;  // tier A: per-column (seed, gamma), updated in place
@@ -450,13 +451,8 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     // ---- walk until few lanes are still walking
     const int live = __popcll(__ballot(true));
     const int stop = (live * A.trav_stop) >> 6;
-    for (;;) {
-      if (__popcll(__ballot(walking)) <= stop) break;
-      if (walking) {
-        walking = trav_step<F>(S, t, kEps, stk, stride, joint, cnt);
-        ready = !walking;
-      }
-    }
+    walk_until<F>(S, t, walking, kEps, stk, stride, joint, stop, (live * A.leaf_stop) >> 6, cnt);
+    ready = !walking;
     if constexpr ((F & F_COUNT) != 0) {
       const unsigned long long s2 = stamp();
       ph_shade += s0b - s0;
@@ -603,8 +599,8 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
   } else {  // the render loop's resumable walk (binary, or 4-wide under F_WIDE)
     Trav t;
     trav_begin<F>(t, r, S.world, tmin, tmax);
-    while (trav_step<F>(S, t, tmin, stk, RT_BLOCK, joint != 0, cnt)) {
-    }
+    bool walking = true;
+    walk_until<F>(S, t, walking, tmin, stk, RT_BLOCK, joint != 0, 0, 0, cnt);
     if (t.tie) {
       trav_restart_ref(t, S.world_ref, tmax);
       while (trav_step<F>(S, t, tmin, stk, RT_BLOCK, joint != 0, cnt)) {
@@ -997,6 +993,10 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   // refill when at most trav_stop/64 of a wave's live lanes still walk (measured: C2 flat at 2-8,
   // -4 % at 16; the 100k-sphere C5 tree, walks ~3x longer, best at 16)
   A.trav_stop = stop_env ? std::max(0, std::min(63, std::atoi(stop_env))) : (c->n_nodes > 20000 ? 16 : 8);
+  const char* leaf_env = std::getenv("RTAMD_LEAF_STOP");
+  // leaf steps once <= that many lanes still seek their first leaf (measured: C2 212.6 ms at 6-8/64
+  // vs 219.7 at 0 and 232 without postponement; C5 (16 spp) 219.9 ms at 16/64 vs 326 at 0)
+  A.leaf_stop = leaf_env ? std::max(0, std::min(64, std::atoi(leaf_env))) : A.trav_stop;
   const unsigned var = variant_for(c->features);
   const bool count = d_work != nullptr;
   // Replacement loop for media-free worlds without instance frames (RTAMD_REPLACE=0 disables),

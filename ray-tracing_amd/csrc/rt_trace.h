@@ -496,6 +496,7 @@ struct Trav {
   double closest_up;  // the test bound: next double above `closest`, so that exact ties are seen
   double best_tmax;   // chain hits: the bound in force when the best hit was found
   int node, sp, best_node, best_sub;
+  int pend;           // F_WIDE: a postponed leaf (flat node id), -1 = none
   bool tie;           // a second leaf hit at exactly `closest`: the walk is redone with `ref`
   bool ref;           // the reference's own walk: caller's tree, left first, bound = closest
   // F_WIDE: the ray in fp32 for the conservative child-box test (wide_keys2)
@@ -523,6 +524,7 @@ __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r, int root, doub
   t.sp = 0;
   t.best_node = -1;
   t.best_sub = 0;
+  t.pend = -1;
   t.tie = false;
   t.ref = false;
   if constexpr ((F & F_WIDE) != 0) {
@@ -568,6 +570,7 @@ __device__ __forceinline__ void trav_restart_ref(Trav& t, int root, double t_max
   t.best_tmax = t_max;
   t.best_node = -1;
   t.best_sub = 0;
+  t.pend = -1;
   t.tie = false;
   t.ref = true;
 }
@@ -710,6 +713,73 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
   if (t.sp == 0) return false;
   t.node = stk[(--t.sp) * stride];
   return true;
+}
+
+// ---- the 4-wide walk with postponed leaves (Aila & Laine's while-while, one postponed slot)
+// A lane keeps stepping wide nodes while it holds one postponed leaf (`pend`); the wave switches to
+// a leaf step, in which every lane holding a leaf tests it, once (almost) no walking lane is still
+// searching for its first leaf. So wide-node steps and fp64 leaf tests do not share a divergent
+// step. Culling is looser while a leaf waits (its hit does not yet bound the walk); the closest
+// hit and the tie flag do not depend on the order leaves are tested in (trav_take).
+constexpr int kNone = (int)0x80000000;  // Trav::node: nothing left but the postponed leaf
+
+__device__ __forceinline__ int trav_pop(Trav& t, const int* stk, int stride) {
+  return t.sp ? stk[(--t.sp) * stride] : kNone;
+}
+// node -> pend when node is a leaf and the slot is free, then continue with the next stack entry
+__device__ __forceinline__ void trav_postpone(Trav& t, const int* stk, int stride) {
+  if (t.node < 0 && t.node != kNone && t.pend < 0) {
+    t.pend = ~t.node;
+    t.node = trav_pop(t, stk, stride);
+  }
+}
+template <unsigned F>
+__device__ __forceinline__ void wide_inner(const Scene& S, Trav& t, int* stk, int stride, Cnt& cnt) {
+  if constexpr ((F & F_COUNT) != 0) ++cnt.wide;
+  if (!wide_node(S, t, stk, stride)) t.node = trav_pop(t, stk, stride);
+  trav_postpone(t, stk, stride);
+}
+template <unsigned F>
+__device__ __forceinline__ void wide_leaf(const Scene& S, Trav& t, double t_min, int* stk, int stride, Cnt& cnt) {
+  if (t.pend >= 0) {
+    trav_leaf<F>(S, t, t.pend, t_min, cnt);
+    t.pend = -1;
+  }
+  trav_postpone(t, stk, stride);
+}
+
+// Step the wave's walking lanes until at most `stop` of them still walk (`walking` goes false when
+// a lane's walk is over). Binary walks: one node per lane per step. 4-wide walks: wide-node steps
+// until at most `leaf_stop` walking lanes still look for their first leaf, then one leaf step.
+template <unsigned F>
+__device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walking, double t_min, int* stk, int stride,
+                                           bool joint, int stop, int leaf_stop, Cnt& cnt) {
+  if constexpr ((F & F_WIDE) == 0) {
+    (void)leaf_stop;
+    for (;;) {
+      if (__popcll(__ballot(walking)) <= stop) break;
+      if (walking) walking = trav_step<F>(S, t, t_min, stk, stride, joint, cnt);
+    }
+  } else {
+    for (;;) {
+      if (__popcll(__ballot(walking)) <= stop) break;
+      // lanes that need wide-node steps before they can test a leaf (tie redo walks: binary steps)
+      const bool seeking = walking && (t.ref || (t.pend < 0 && t.node >= 0));
+      const bool holding = walking && !t.ref && t.pend >= 0;
+      // (every walking lane is seeking or holding, so one of the two steps always makes progress)
+      if (__popcll(__ballot(seeking)) > leaf_stop || __ballot(holding) == 0) {
+        if (walking && t.ref) {
+          walking = trav_step<F>(S, t, t_min, stk, stride, joint, cnt);
+        } else if (walking && t.node >= 0) {
+          wide_inner<F>(S, t, stk, stride, cnt);
+          walking = t.node != kNone || t.pend >= 0;
+        }
+      } else if (holding) {
+        wide_leaf<F>(S, t, t_min, stk, stride, cnt);
+        walking = t.node != kNone || t.pend >= 0;
+      }
+    }
+  }
 }
 
 // The closest hit's record, built once from the same ray with the same operations (a chain

@@ -120,12 +120,27 @@ class RTError(RuntimeError):
     pass
 
 
+def _share_torch_hip_runtime():
+    """One HIP runtime per process. PyTorch-ROCm ships its own libamdhip64 (soname
+    libamdhip64.so.7, like /opt/rocm's). If librtamd.so were loaded first, its DT_NEEDED would pull
+    /opt/rocm's copy and torch would later map a second runtime that finds no GPU. Loading torch's
+    copy globally first makes librtamd bind to it (same soname), whichever is imported first."""
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return
+    hip = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(hip):
+        C.CDLL(hip, mode=C.RTLD_GLOBAL)
+
+
 def lib() -> C.CDLL:
     """Load librtamd.so (raises if it has not been built: there is no fallback)."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RTError(f"librtamd.so not found at {LIB_PATH}; run __graft_entry__.build() / make")
+        _share_torch_hip_runtime()
         L = C.CDLL(LIB_PATH)
         D, I, U64 = C.c_double, C.c_int, C.c_uint64
         P = C.POINTER
