@@ -238,7 +238,7 @@ def main():
         }
         cb = None
         counters = None
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU leg is timed at N=1 only
             if not args.cpu_spp:
                 args.cpu_spp = max(1, min(cfg["spp"], round(40e6 / (cfg["W"] * cfg["H"]))))
             v, dt, counters = cpu_baseline(cfg, scene, cam, args.cpu_threads, args.cpu_spp)

@@ -908,7 +908,8 @@ const void* pick(int loop, bool lds, int w, bool count) {
 const void* philox_kernel(unsigned var, int loop, bool lds, int w, bool count) {
   if (var == kVarSpheres) return pick<kVarSpheres>(loop, lds, w, count);
   if (var == kVarCornell) return pick<kVarCornell>(loop, lds, w, count);
-  return count ? (const void*)render_philox<F_ALL | F_COUNT, 1> : (const void*)render_philox<F_ALL, 1>;
+  if (count) return (const void*)render_philox<F_ALL | F_COUNT, 1>;
+  return w >= 2 ? (const void*)render_philox<F_ALL, 2> : (const void*)render_philox<F_ALL, 1>;
 }
 bool env_off(const char* name) {
   const char* e = std::getenv(name);
@@ -1011,7 +1012,9 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   const int loop = wide ? 2 : (replace ? 1 : 0);
   // waves per SIMD (measured, C2 / C3): spheres 3 (W=2: -11 %); Cornell 2 on the replacement
   // loop (578 vs 409 Msamples/s at 1), 1 on the per-sample loop
-  const int waves = var == kVarSpheres ? waves_target(3) : waves_target(loop ? 2 : 1);
+  // full variant (media/frames, per-sample loop): 2 waves despite 784 B/lane of scratch (C4 at 50
+  // spp: 35.2 vs 23.4 Msamples/s at 1 wave (457 registers), 9.1 at 3)
+  const int waves = var == kVarSpheres ? waves_target(3) : waves_target(loop || var == F_ALL ? 2 : 1);
   // LDS-staged kernel when the traversal's node array plus the stacks fit one CU's 160 KiB
   // (RTAMD_LDS=0 disables it for A/B runs).
   if (!count && !env_off("RTAMD_LDS") && var != F_ALL) {

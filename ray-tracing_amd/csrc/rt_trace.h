@@ -351,15 +351,34 @@ __device__ inline bool chain_hit(const Scene& S, int id, const Ray& ray, double 
   return true;
 }
 
-// hit ConstantMedium (Lib.hs:1053-1080). The boundary is a primitive chain (host-validated).
+// The t of a chain hit only: Translate/Rotate move and rotate the ray, which keeps its parameter,
+// so the chain's t is its primitive's t in the innermost frame (the same operations chain_hit runs).
+template <unsigned F>
+__device__ inline bool chain_t(const Scene& S, int id, const Ray& ray, double t_min, double t_max, double& t) {
+  Ray r = ray;
+  int cur = id;
+  if constexpr ((F & F_INST) != 0) {
+    while (true) {
+      const int type = S.nodes[cur].type & RT_TYPE_MASK;
+      if (type != RT_NODE_TRANSLATE && type != RT_NODE_ROTATE) break;
+      r = enter_instance(&S.nodes[cur], r);
+      cur = S.nodes[cur].a;
+    }
+  }
+  int sub;
+  return prim_t<F>(S, &S.nodes[cur], prep(r), t_min, t_max, t, sub);
+}
+
+// hit ConstantMedium (Lib.hs:1053-1080). The boundary is a primitive chain (host-validated); only
+// the two boundary hits' t are used.
 template <unsigned F, class R>
 __device__ inline bool medium_hit(const Scene& S, const rt_node* n, const Ray& r, double t_min, double t_max, R& g,
                                   Hit& h) {
-  Hit h1, h2;
-  if (!chain_hit<F>(S, n->a, r, -INFINITY, INFINITY, h1)) return false;
-  if (!chain_hit<F>(S, n->a, r, h1.t + kEps, INFINITY, h2)) return false;
-  const double rec1tp = gmax(t_min, h1.t);
-  const double rec2t = gmin(t_max, h2.t);
+  double t1, t2;
+  if (!chain_t<F>(S, n->a, r, -INFINITY, INFINITY, t1)) return false;
+  if (!chain_t<F>(S, n->a, r, t1 + kEps, INFINITY, t2)) return false;
+  const double rec1tp = gmax(t_min, t1);
+  const double rec2t = gmin(t_max, t2);
   if (rec1tp >= rec2t) return false;
   const double rec1t = rec1tp < 0 ? 0 : rec1tp;
   const double ray_length = vlen(r.d);

@@ -111,8 +111,6 @@ def test_gpu_cornell_tier_a_golden(gpu_ctx):
 @pytest.mark.parametrize("walk", [0, rtamd.RT_DEBUG_RESUMABLE, rtamd.RT_DEBUG_WIDE])
 @pytest.mark.parametrize("name", ["random_book_one", "cornell"])
 def test_gpu_closest_hits_golden(gpu_ctx, name, walk):
-    if walk == rtamd.RT_DEBUG_WIDE and name == "cornell":
-        pytest.skip("no 4-wide tree for an 8-leaf world (not rebuilt)")
     sc, _ = rtamd.make_scene(name, rtamd.randGen(1024))
     gpu_ctx.upload(sc)
     got = gpu_ctx.closest_hits(G[f"hits_{name}_rays"], 1e-4, np.inf, seed=3, flags=walk)
