@@ -250,6 +250,12 @@ def main():
         if work:
             n = max(1, work["samples"])
             out["phase_split"] = {k: round(v, 4) for k, v in work.pop("phase_split").items()}
+            slots = work.pop("lane_slots")
+            if slots["outer_iterations"]:  # lane utilisation of the replacement loop's phases
+                out["lane_utilisation"] = {
+                    "wide_steps": round(work["wide_nodes"] / max(1, slots["wide_steps"]), 4),
+                    "leaf_steps": round(work["prim_tests"] / max(1, slots["leaf_steps"]), 4),
+                    "shade": round(work["segments"] / max(1, slots["outer_iterations"]), 4)}
             per = {k: work[k] / n for k in work}
             bytes_per_sample = sum(BYTES[k] * per[k] for k in BYTES) + 3.0 / cfg["spp"]
             flops_per_sample = sum(FLOPS[k] * per[k] for k in FLOPS)

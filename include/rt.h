@@ -351,7 +351,9 @@ int rt_assemble_linear_async(rt_ctx* ctx, const rt_render_params* p, const doubl
  * roofline. out_work[0..7] = {segments traced, BVH box tests, leaf primitive tests,
  * instance/medium tests, light-pdf evaluations, Philox blocks, samples, 4-wide node visits}
  * for this shard; out_work[8..10] = wave time (s_memtime ticks, summed over waves) spent acquiring work and
- * starting samples / traversing / shading; the rest 0.
+ * starting samples / traversing / shading; out_work[11..13] (ray-replacement loop only) = live-lane
+ * slots of 4-wide node steps, of leaf steps and of outer iterations (lane utilisation = work / slots);
+ * the rest 0.
  */
 int rt_render_work(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* p, uint64_t out_work[16]);
 

@@ -380,7 +380,10 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
 
   for (;;) {
     unsigned long long s0 = 0;
-    if constexpr ((F & F_COUNT) != 0) s0 = stamp();
+    if constexpr ((F & F_COUNT) != 0) {
+      s0 = stamp();
+      ++cnt.oslot;
+    }
     // ---- shade finished walks, then set up the next walk for every lane that is not walking
     if (ready && t.tie) {  // exact tie: redo this walk as the reference does
       ready = false;
@@ -469,6 +472,9 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     wave_add(&A.work[5], blocks);
     wave_add(&A.work[6], samples);
     wave_add(&A.work[7], cnt.wide);
+    wave_add(&A.work[11], cnt.islot);
+    wave_add(&A.work[12], cnt.lslot);
+    wave_add(&A.work[13], cnt.oslot);
     if ((threadIdx.x & 63) == 0) {
       atomicAdd(&A.work[8], ph_setup);
       atomicAdd(&A.work[9], ph_trav);
@@ -1019,7 +1025,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   // (RTAMD_LDS=0 disables it for A/B runs).
   if (!count && !env_off("RTAMD_LDS") && var != F_ALL) {
     const int block = waves * 256;
-    const int entries = (wide ? c->wide_stack_need : c->stack_need) + 2;
+    const int entries = wide ? c->wide_stack_need + 3 : c->stack_need + 2;  // (wide_node writes 3 slots)
     const int items = wide ? c->n_wnodes : c->n_nodes;
     const size_t rec = wide ? sizeof(rt_wnode) : sizeof(rt_node);
     const size_t bytes = (size_t)items * rec + (size_t)entries * block * sizeof(int);
@@ -1184,7 +1190,7 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
   if (c->replace_ok) {  // 4-wide fp32-box tree over the same world tree (unflagged node copy)
     std::vector<rt_wnode> wide;
     int need = 0;
-    if (rt::build_wide_bvh(nodes, d->world_root, wide, &need) && need + 2 <= RT_WSTACK &&
+    if (rt::build_wide_bvh(nodes, d->world_root, wide, &need) && need + 3 <= RT_WSTACK &&
         (size_t)wide.size() < (size_t)INT32_MAX / 2) {
       if ((rc = upload(&c->d_wnodes, wide.data(), wide.size()))) {
         free_scene(c);

@@ -21,6 +21,7 @@ enum : unsigned {
 // Work counters of the counting build (F_COUNT); all zero-cost otherwise.
 struct Cnt {
   unsigned box, prim, other, light, wide;
+  unsigned islot, lslot, oslot;  // lane slots (live lanes) of wide-node steps, leaf steps, outer iterations
 };
 
 // ------------------------------------------------------------------ textures (Lib.hs:441-513)
@@ -692,12 +693,16 @@ __device__ __forceinline__ bool wide_node(const Scene& S, Trav& t, int* stk, int
   cswap(k0, c0, k2, c2);
   cswap(k1, c1, k3, c3);
   cswap(k1, c1, k2, c2);
-  if (n_hit == 0) return false;
-  if (n_hit > 3) stk[(t.sp++) * stride] = c3;
-  if (n_hit > 2) stk[(t.sp++) * stride] = c2;
-  if (n_hit > 1) stk[(t.sp++) * stride] = c1;
+  // Stack the accepted children after c0 without branches, farthest deepest: three slots are always
+  // written (slots at or above the new sp are dead; the stacks have 3 entries of headroom for this).
+  const int e0 = n_hit > 3 ? c3 : (n_hit > 2 ? c2 : c1);
+  const int e1 = n_hit > 3 ? c2 : c1;
+  stk[t.sp * stride] = e0;
+  stk[(t.sp + 1) * stride] = e1;
+  stk[(t.sp + 2) * stride] = c1;
+  t.sp += n_hit > 1 ? n_hit - 1 : 0;
   t.node = c0;
-  return true;
+  return n_hit != 0;
 }
 
 // Visit one node; false once the walk is over.
@@ -787,15 +792,19 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
       const bool holding = walking && !t.ref && t.pend >= 0;
       // (every walking lane is seeking or holding, so one of the two steps always makes progress)
       if (__popcll(__ballot(seeking)) > leaf_stop || __ballot(holding) == 0) {
+        if constexpr ((F & F_COUNT) != 0) ++cnt.islot;
         if (walking && t.ref) {
           walking = trav_step<F>(S, t, t_min, stk, stride, joint, cnt);
         } else if (walking && t.node >= 0) {
           wide_inner<F>(S, t, stk, stride, cnt);
           walking = t.node != kNone || t.pend >= 0;
         }
-      } else if (holding) {
-        wide_leaf<F>(S, t, t_min, stk, stride, cnt);
-        walking = t.node != kNone || t.pend >= 0;
+      } else {
+        if constexpr ((F & F_COUNT) != 0) ++cnt.lslot;
+        if (holding) {
+          wide_leaf<F>(S, t, t_min, stk, stride, cnt);
+          walking = t.node != kNone || t.pend >= 0;
+        }
       }
     }
   }

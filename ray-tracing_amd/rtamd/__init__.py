@@ -503,6 +503,8 @@ class Context:
         out = dict(zip(self.WORK_FIELDS, [int(x) for x in w[:8]]))
         tot = max(1, int(w[8]) + int(w[9]) + int(w[10]))
         out["phase_split"] = {"acquire_camera": int(w[8]) / tot, "traverse": int(w[9]) / tot, "shade": int(w[10]) / tot}
+        # replacement loop only: live-lane slots of 4-wide node steps, leaf steps and outer iterations
+        out["lane_slots"] = {"wide_steps": int(w[11]), "leaf_steps": int(w[12]), "outer_iterations": int(w[13])}
         return out
 
     def last_kernel_ms(self) -> float:
