@@ -152,6 +152,7 @@ __device__ __forceinline__ double word_to_draw(uint64_t w) {
 // Tier A: the reference's SplitMix64 stream (nextWord64).
 struct RngExact {
   uint64_t seed, gamma;
+  __device__ __forceinline__ void reserve(int) {}
   __device__ __forceinline__ double draw() {
     seed += gamma;
     return word_to_draw(mix64(seed));
@@ -173,32 +174,53 @@ __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) 
     k1 += 0xBB67AE85u;
   }
 }
+// The stream's words pass through a 4-word FIFO. `reserve(k)` tops it up to k words, one Philox
+// block per loop trip, at a point where the whole wave runs the same code; `draw` then only shifts
+// the FIFO. (Blocks computed inside every divergent draw site would each cost the wave a full
+// Philox evaluation.) The sequence of words is the stream's, whatever the reserve points.
 struct RngPhilox {
   uint32_t k0, k1, pid, sample, pair;
-  uint32_t have;
-  uint64_t spare;
+  uint32_t n;  // buffered words
+  uint64_t w0, w1, w2, w3;
   __device__ __forceinline__ void init(uint64_t seed, uint32_t p, uint32_t s) {
     k0 = (uint32_t)seed;
     k1 = (uint32_t)(seed >> 32);
     pid = p;
     sample = s;
     pair = 0;
-    have = 0;
-    spare = 0;
+    n = 0;
+  }
+  __device__ __forceinline__ void block(uint64_t& x, uint64_t& y) {
+    uint32_t c[4] = {pair, sample, pid, 0u};
+    philox(c, k0, k1);
+    ++pair;
+    x = (uint64_t)c[0] | ((uint64_t)c[1] << 32);
+    y = (uint64_t)c[2] | ((uint64_t)c[3] << 32);
+  }
+  __device__ __forceinline__ void reserve(int k) {  // k <= 3 (the FIFO then holds at most 4 words)
+    while ((int)n < k) {
+      uint64_t x, y;
+      block(x, y);
+      if (n == 0) {
+        w0 = x;
+        w1 = y;
+      } else if (n == 1) {
+        w1 = x;
+        w2 = y;
+      } else {
+        w2 = x;
+        w3 = y;
+      }
+      n += 2;
+    }
   }
   __device__ __forceinline__ double draw() {
-    uint64_t w;
-    if (have) {
-      have = 0;
-      w = spare;
-    } else {
-      uint32_t c[4] = {pair, sample, pid, 0u};
-      philox(c, k0, k1);
-      ++pair;
-      w = (uint64_t)c[0] | ((uint64_t)c[1] << 32);
-      spare = (uint64_t)c[2] | ((uint64_t)c[3] << 32);
-      have = 1;
-    }
+    if (n == 0) block(w0, w1), n = 2;  // not reserved: compute here
+    const uint64_t w = w0;
+    w0 = w1;
+    w1 = w2;
+    w2 = w3;
+    --n;
     return word_to_draw(w);
   }
 };
@@ -211,6 +233,7 @@ __device__ __forceinline__ double draw_r(R& g, double mn, double mx) {  // rando
 template <class R>
 __device__ __forceinline__ V3 random_in_unit_sphere(R& g) {  // Lib.hs:1160-1168
   for (;;) {
+    g.reserve(3);
     const double x = g.draw(), y = g.draw(), z = g.draw();
     const V3 p = scale(2.0, v3(x, y, z)) - v3(1.0, 1.0, 1.0);
     if (sqlen(p) < 1.0) return p;
@@ -219,6 +242,7 @@ __device__ __forceinline__ V3 random_in_unit_sphere(R& g) {  // Lib.hs:1160-1168
 template <class R>
 __device__ __forceinline__ V3 random_in_unit_disk(R& g) {  // Lib.hs:1178-1185
   for (;;) {
+    g.reserve(2);
     const double x = g.draw(), y = g.draw();
     const V3 p = scale(2.0, v3(x, y, 0.0)) - v3(1.0, 1.0, 0.0);
     if (sqlen(p) < 1.0) return p;

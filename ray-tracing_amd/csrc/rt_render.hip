@@ -112,6 +112,7 @@ template <class R>
 __device__ __forceinline__ Ray get_ray(const rt_camera& k, double s, double t, R& g) {
   const V3 rd = scale(k.lens_radius, random_in_unit_disk(g));
   const V3 offset = scale(rd.x, vload(k.u)) + scale(rd.y, vload(k.v));
+  g.reserve(1);
   const double tm = draw_r(g, k.t0, k.t1);
   Ray r;
   r.o = vload(k.origin) + offset;
@@ -261,6 +262,7 @@ __device__ __forceinline__ void philox_loop(const RenderArgs& A, const Scene& S,
     if (!path) {  // start sample s: uniformRandomUVs' pair, then getRay
       const uint32_t pid = (uint32_t)((long long)row * A.W + px);
       g.init(A.seed, pid, (uint32_t)s);
+      g.reserve(3);  // the UV pair and the first disk try
       const double ru = g.draw(), rv = g.draw();
       const int y = A.H - 1 - row;
       const double u = ((double)px + ru) / (double)A.W;
@@ -433,6 +435,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
       // start sample s: uniformRandomUVs' pair, then getRay
       const uint32_t pid = (uint32_t)((long long)row * A.W + px);
       g.init(A.seed, pid, (uint32_t)s);
+      g.reserve(3);  // the UV pair and the first disk try
       const double ru = g.draw(), rv = g.draw();
       const int y = A.H - 1 - row;
       const double u = ((double)px + ru) / (double)A.W;

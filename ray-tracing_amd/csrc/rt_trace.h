@@ -913,6 +913,7 @@ template <unsigned F, class R>
 __device__ __forceinline__ void scatter(const Scene& S, const DMat& m, const Ray& r, const Hit& h, R& g, Scatter& s) {
   s.ray.o = h.p;
   s.ray.tm = r.tm;
+  g.reserve(3);  // Lambertian draws 1 or 3 (more when sampling a lights BVH), Metal 2, Dielectric 1
   if (m.type == RT_MAT_LAMBERTIAN) {  // Lib.hs:823-836, mixture of light and cosine pdfs
     s.att = texture_value<F>(S, m.tex, h.u, h.v, h.p);
     const ONB uvw = onb_from_w(h.n);
