@@ -1019,11 +1019,12 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   const bool want_wide = wenv ? wenv[0] != '0' : c->rebuilt_bvh;
   const bool wide = replace && c->d_wnodes && !(p->flags & RT_FLAG_REFERENCE_CULL) && want_wide;
   const int loop = wide ? 2 : (replace ? 1 : 0);
-  // waves per SIMD (measured, C2 / C3): spheres 3 (W=2: -11 %); Cornell 2 on the replacement
-  // loop (578 vs 409 Msamples/s at 1), 1 on the per-sample loop
-  // full variant (media/frames, per-sample loop): 2 waves despite 784 B/lane of scratch (C4 at 50
-  // spp: 35.2 vs 23.4 Msamples/s at 1 wave (457 registers), 9.1 at 3)
-  const int waves = var == kVarSpheres ? waves_target(3) : waves_target(loop || var == F_ALL ? 2 : 1);
+  // waves per SIMD (measured): spheres 3 (C2 -11 % at 2, -9 % at 4; C5 -15 % at 2); Cornell-like
+  // on the replacement loop 3 (C3 380.5 ms vs 453.7 at 2, 428.6 at 4), 1 on the per-sample loop;
+  // full variant (media/frames, per-sample loop) 2 despite 784 B/lane of scratch (C4 at 50 spp:
+  // 35.2 vs 23.4 Msamples/s at 1 wave (457 registers), 9.1 at 3)
+  const int waves = (var == kVarSpheres || (var == kVarCornell && loop)) ? waves_target(3)
+                                                                          : waves_target(var == F_ALL ? 2 : 1);
   // LDS-staged kernel when the traversal's node array plus the stacks fit one CU's 160 KiB
   // (RTAMD_LDS=0 disables it for A/B runs).
   if (!count && !env_off("RTAMD_LDS") && var != F_ALL) {
