@@ -58,17 +58,31 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(cfg, scene, cam, threads, spp_sample):
-    """The oracle (C restatement, tier-B streams) on a bounded sample of the same frame: every
-    pixel, samples 0..spp_sample-1. Also yields the per-sample work counters."""
+def cpu_baseline(cfg, scene, cam, threads, spp_sample, budget_s=10.0):
+    """The oracle (C restatement, tier-B streams) on a bounded sample of the same frame: samples
+    0..spp-1 of every pixel of a band of rows around the middle of the image. A 1-spp probe of a
+    thin band sizes the sample to about `budget_s` seconds (scenes differ ~100x in CPU cost per
+    sample); `spp_sample` caps its spp. Also yields the per-sample work counters."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
-    p = rtamd.make_params(cfg["W"], cfg["H"], spp_sample, cfg["depth"], rtamd.RT_RNG_PHILOX, seed=1024)
-    t0 = time.perf_counter()
-    _, _, _, cnt = pyoracle.render(scene, cam, p, nthreads=threads, linear=False, counters=True)
-    dt = time.perf_counter() - t0
-    samples = cfg["W"] * cfg["H"] * spp_sample
-    return samples / dt / 1e6, dt, cnt
+    W, H = cfg["W"], cfg["H"]
+
+    def run(rows, spp):
+        r0 = (H - rows) // 2
+        p = rtamd.make_params(W, H, spp, cfg["depth"], rtamd.RT_RNG_PHILOX, seed=1024)
+        t0 = time.perf_counter()
+        _, _, _, cnt = pyoracle.render(scene, cam, p, rows=(r0, r0 + rows), nthreads=threads, linear=False,
+                                       counters=True)
+        return time.perf_counter() - t0, cnt, r0
+
+    probe_rows = max(1, min(H, round(2e5 / W)))
+    dt, _, _ = run(probe_rows, 1)
+    rate = probe_rows * W / max(dt, 1e-6)  # samples/s
+    n = rate * budget_s
+    spp = int(max(1, min(spp_sample, n // (W * H))))
+    rows = int(max(1, min(H, n // (W * spp))))
+    dt, cnt, r0 = run(rows, spp)
+    return rows * W * spp / dt / 1e6, dt, cnt, f"rows {r0}..{r0 + rows - 1} of {H} (all {W} columns) at {spp} spp"
 
 
 def cpu_model():
@@ -116,7 +130,7 @@ def main():
     ap.add_argument("--tile", type=int, default=16)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     ap.add_argument("--cpu-spp", type=int, default=0,
-                    help="spp of the bounded CPU sample (default: ~40 M samples, ~10 s on 16 cores)")
+                    help="spp cap of the bounded CPU sample (default min(spp, 40M/(W*H)); a probe sizes the sample to ~10 s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-work", action="store_true", help="skip the counting-build pass")
     ap.add_argument("--traffic-json", default="",
@@ -241,11 +255,11 @@ def main():
         if not args.no_cpu_baseline and world == 1:  # the CPU leg is timed at N=1 only
             if not args.cpu_spp:
                 args.cpu_spp = max(1, min(cfg["spp"], round(40e6 / (cfg["W"] * cfg["H"]))))
-            v, dt, counters = cpu_baseline(cfg, scene, cam, args.cpu_threads, args.cpu_spp)
+            v, dt, counters, what = cpu_baseline(cfg, scene, cam, args.cpu_threads, args.cpu_spp)
             cb = {"value": round(v, 4), "unit": "Msamples/s", "cores": args.cpu_threads, "kind": "port",
                   "cpu": cpu_model(),
-                  "sample": f"full {cfg['W']}x{cfg['H']} frame at {args.cpu_spp} spp (tier-B streams 0..{args.cpu_spp - 1}"
-                            f" of every pixel), {dt:.1f} s, oracle/oracle.c fp64 glibc -O2 OpenMP"}
+                  "sample": f"{what} (tier-B streams of the same frame), {dt:.1f} s, oracle/oracle.c fp64 glibc "
+                            f"-O2 OpenMP"}
         out["cpu_baseline"] = cb
         if work:
             n = max(1, work["samples"])
