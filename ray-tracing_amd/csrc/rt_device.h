@@ -21,6 +21,7 @@
 #define RT_WSTACK 48 /* the same for the 4-wide walk (up to 3 siblings stacked per level) */
 #endif
 #define RT_LIGHT_DEPTH 2  /* max BVH depth of the lights tree (host-validated) */
+#define RT_MAX_FRAMES 4   /* max nesting of instance frames on the replacement loop (host-validated) */
 #define RT_FRAME 0x40000000 /* stack-entry tag: instance frame marker */
 #define RT_CHAIN_PRIM 0x100 /* device node type flag: Translate/Rotate chain ending in a primitive */
 #define RT_TYPE_MASK 0xff
@@ -135,6 +136,8 @@ struct Scene {
   int world;
   int world_ref;  // the caller's (makeBVH) world root: exact ties are resolved on this tree
   int lights;
+  int ref_walk;   // media or instance frames: the replacement loop walks the caller's tree in the
+                  // reference's own order (media draw order, Lib.hs:971-988,1053-1080)
   double bg[3];
 };
 

@@ -350,7 +350,7 @@ __global__ void __launch_bounds__(WAVES * 256, WAVES) render_philox_lds(RenderAr
 // node at a time until at most trav_stop/64 of the live lanes are still walking. Lanes never
 // wait for the slowest walk of their wave, and shading runs for many lanes at once.
 template <unsigned F>
-__device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S, int* stk, int stride) {
+__device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S, int* stk, int stride, int* side_p) {
   const int lane = threadIdx.x & 63;
   const unsigned long long lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const bool joint = !(A.flags & RT_FLAG_REFERENCE_CULL);
@@ -362,6 +362,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
   RngPhilox g;
   g.init(A.seed, 0, 0);
   Trav t;  // the segment's ray lives only here between segments (no second copy is carried)
+  Side side{side_p, stride};
   Cnt cnt{0, 0, 0, 0, 0};
   unsigned long long segs = 0, blocks = 0, samples = 0, ph_setup = 0, ph_trav = 0, ph_shade = 0;
 
@@ -395,8 +396,8 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     if (ready) {
       ready = false;
       Hit h;
-      Ray ray = plain(t.ray);
-      const bool got = trav_finish<F>(S, t, ray, kEps, h);
+      Ray ray = plain(t.ray);  // (every frame has closed: the world ray again)
+      const bool got = trav_finish<F>(S, t, ray, kEps, h, side);
       V3 contrib;
       if (shade_hit<F>(S, got, h, ray, thr, depth, g, contrib, cnt)) {
         end_sample(contrib);
@@ -404,6 +405,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
         end_sample(vmul(thr, v3(0.0, 0.0, 0.0)));
       } else {  // next segment of the same path
         trav_begin<F>(t, ray, S.world, kEps, INFINITY);
+        if (S.ref_walk) trav_restart_ref(t, S.world_ref, INFINITY);
         walking = true;
         if constexpr ((F & F_COUNT) != 0) ++segs;
       }
@@ -448,6 +450,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
         continue;
       }
       trav_begin<F>(t, ray, S.world, kEps, INFINITY);
+      if (S.ref_walk) trav_restart_ref(t, S.world_ref, INFINITY);
       walking = true;
       if constexpr ((F & F_COUNT) != 0) ++segs;
     }
@@ -457,7 +460,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     // ---- walk until few lanes are still walking
     const int live = __popcll(__ballot(true));
     const int stop = (live * A.trav_stop) >> 6;
-    walk_until<F>(S, t, walking, kEps, stk, stride, joint, stop, (live * A.leaf_stop) >> 6, cnt);
+    walk_until<F>(S, t, walking, kEps, stk, stride, joint, stop, (live * A.leaf_stop) >> 6, cnt, g, side);
     ready = !walking;
     if constexpr ((F & F_COUNT) != 0) {
       const unsigned long long s2 = stamp();
@@ -486,10 +489,17 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
   }
 }
 
+// LDS ints per lane of a kernel: the traversal stack, then (instance frames possible) Side slots
+template <unsigned F>
+constexpr int lane_ints() {
+  return ((F & F_WIDE) ? RT_WSTACK : RT_STACK) + ((F & F_FRAMES) ? kSideInts : 0);
+}
+
 template <unsigned F, int WAVES>
 __global__ void __launch_bounds__(RT_BLOCK, WAVES) render_philox2(RenderArgs A) {
-  __shared__ int stk_mem[((F & F_WIDE) ? RT_WSTACK : RT_STACK) * RT_BLOCK];
-  philox_loop2<F>(A, A.S, &stk_mem[threadIdx.x], RT_BLOCK);
+  __shared__ int stk_mem[lane_ints<F>() * RT_BLOCK];
+  constexpr int stack = (F & F_WIDE) ? RT_WSTACK : RT_STACK;
+  philox_loop2<F>(A, A.S, &stk_mem[threadIdx.x], RT_BLOCK, &stk_mem[stack * RT_BLOCK + threadIdx.x]);
 }
 
 // LDS-staged replacement loop: the traversal's node array (the wide records for F_WIDE, else the
@@ -511,8 +521,9 @@ __global__ void __launch_bounds__(WAVES * 256, WAVES) render_philox2_lds(RenderA
   if constexpr ((F & F_WIDE) != 0) S.wnodes = reinterpret_cast<const rt_wnode*>(lds);
   else S.nodes = reinterpret_cast<const rt_node*>(lds);
   int* stk = reinterpret_cast<int*>(lds + (size_t)n_nodes * rec) + threadIdx.x;
-  (void)stack_entries;
-  philox_loop2<F>(A, S, stk, WAVES * 256);
+  // (the host sizes the dynamic LDS for stack_entries stack ints + kSideInts Side ints per lane
+  // when F has F_FRAMES)
+  philox_loop2<F>(A, S, stk, WAVES * 256, stk + stack_entries * WAVES * 256);
 }
 
 // Tier B: a slab pixel's chunk sums added in chunk order, then averaged and stored (rt.h).
@@ -591,8 +602,9 @@ __global__ void assemble(const T* slabs, T* image, int W, int H, int tile, int t
 template <unsigned F>
 __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* rays, int n, double tmin,
                                                          double tmax, uint64_t seed, int joint, int walk, double* out) {
-  __shared__ int stk_mem[((F & F_WIDE) ? RT_WSTACK : RT_STACK) * RT_BLOCK];
+  __shared__ int stk_mem[lane_ints<F>() * RT_BLOCK];
   int* stk = &stk_mem[threadIdx.x];
+  Side side{&stk_mem[((F & F_WIDE) ? RT_WSTACK : RT_STACK) * RT_BLOCK + threadIdx.x], RT_BLOCK};
   const int i = blockIdx.x * RT_BLOCK + threadIdx.x;
   if (i >= n) return;
   const double* q = rays + 7 * (long long)i;
@@ -608,14 +620,15 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
   } else {  // the render loop's resumable walk (binary, or 4-wide under F_WIDE)
     Trav t;
     trav_begin<F>(t, r, S.world, tmin, tmax);
+    if (S.ref_walk) trav_restart_ref(t, S.world_ref, tmax);
     bool walking = true;
-    walk_until<F>(S, t, walking, tmin, stk, RT_BLOCK, joint != 0, 0, 0, cnt);
+    walk_until<F>(S, t, walking, tmin, stk, RT_BLOCK, joint != 0, 0, 0, cnt, g, side);
     if (t.tie) {
       trav_restart_ref(t, S.world_ref, tmax);
-      while (trav_step<F>(S, t, tmin, stk, RT_BLOCK, joint != 0, cnt)) {
+      while (trav_step<F>(S, t, tmin, stk, RT_BLOCK, joint != 0, cnt, g, side)) {
       }
     }
-    got = trav_finish<F>(S, t, r, tmin, h);
+    got = trav_finish<F>(S, t, r, tmin, h, side);
   }
   if (got) {
     o[0] = 1; o[1] = h.t;
@@ -673,7 +686,7 @@ struct rt_ctx {
   int n_wnodes = 0;
   int wide_stack_need = 0;
   bool rebuilt_bvh = false;
-  bool replace_ok = false;  // media-free and no instance frames: the replacement loop applies
+  bool replace_ok = false;  // frames nest <= RT_MAX_FRAMES deep: the replacement loop applies
   bool has_scene = false;
   unsigned long long* d_counter = nullptr;
   double* d_partial = nullptr;  // tier-B chunk sums (grown on demand)
@@ -729,7 +742,7 @@ bool is_leaf_prim(int type) {
 struct Validator {
   const rt_scene_desc* d;
   std::vector<rt_node> nodes;  // device copy (type flags added)
-  std::vector<int> stack_need, chain_prim;
+  std::vector<int> stack_need, chain_prim, frame_depth;  // frame_depth: nesting of instance frames
   std::string err;
 
   bool child_ok(int parent, int child) { return child >= 0 && child < parent; }
@@ -740,6 +753,7 @@ struct Validator {
     nodes.assign(d->nodes, d->nodes + n);
     stack_need.assign(n, 0);
     chain_prim.assign(n, 0);
+    frame_depth.assign(n, 0);
     for (int i = 0; i < n; ++i) {
       rt_node& x = nodes[i];
       const int t = x.type;
@@ -748,6 +762,7 @@ struct Validator {
           if (!child_ok(i, x.a) || !child_ok(i, x.b)) return fail("BVH child must precede its parent");
           if (x.c <= 0) return fail("BVH size must be positive");
           stack_need[i] = std::max(1 + stack_need[x.a], stack_need[x.b]);
+          frame_depth[i] = std::max(frame_depth[x.a], frame_depth[x.b]);
           break;
         case RT_NODE_SPHERE:
         case RT_NODE_RECT_XY:
@@ -771,6 +786,7 @@ struct Validator {
             x.type |= RT_CHAIN_PRIM;
           } else {
             stack_need[i] = 1 + stack_need[x.a];
+            frame_depth[i] = 1 + frame_depth[x.a];
           }
           break;
         case RT_NODE_CONSTANT_MEDIUM:
@@ -917,7 +933,14 @@ const void* pick(int loop, bool lds, int w, bool count) {
 const void* philox_kernel(unsigned var, int loop, bool lds, int w, bool count) {
   if (var == kVarSpheres) return pick<kVarSpheres>(loop, lds, w, count);
   if (var == kVarCornell) return pick<kVarCornell>(loop, lds, w, count);
-  if (count) return (const void*)render_philox<F_ALL | F_COUNT, 1>;
+  // full variant (media, frames, textures, motion): ray replacement over the caller's tree in the
+  // reference's order (loop 1), or the per-sample loop (loop 0)
+  if (count)
+    return loop ? (const void*)render_philox2<F_ALL | F_COUNT, 1> : (const void*)render_philox<F_ALL | F_COUNT, 1>;
+  if (loop) {
+    if (lds) return w >= 3 ? (const void*)render_philox2_lds<F_ALL, 3> : (const void*)render_philox2_lds<F_ALL, 2>;
+    return w >= 3 ? (const void*)render_philox2<F_ALL, 3> : (const void*)render_philox2<F_ALL, 2>;
+  }
   return w >= 2 ? (const void*)render_philox<F_ALL, 2> : (const void*)render_philox<F_ALL, 1>;
 }
 bool env_off(const char* name) {
@@ -1009,30 +1032,32 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   A.leaf_stop = leaf_env ? std::max(0, std::min(64, std::atoi(leaf_env))) : A.trav_stop;
   const unsigned var = variant_for(c->features);
   const bool count = d_work != nullptr;
-  // Replacement loop for media-free worlds without instance frames (RTAMD_REPLACE=0 disables),
-  // over the 4-wide tree when one was built (RTAMD_WIDE=0 disables; the reference-cull flag
-  // asks for the binary tree's exact box test).
-  const bool replace = c->replace_ok && var != F_ALL && !env_off("RTAMD_REPLACE");
+  // Replacement loop (RTAMD_REPLACE=0 disables) for every world whose instance frames nest at most
+  // RT_MAX_FRAMES deep; worlds with media or frames walk the caller's tree in the reference's order.
+  // Over the 4-wide tree when one was built (RTAMD_WIDE=0 disables; the reference-cull flag asks
+  // for the binary tree's exact box test).
+  const bool replace = c->replace_ok && !env_off("RTAMD_REPLACE");
   // The wide tree pays off on rebuilt (>= 16-leaf) worlds; small worlds keep the binary walk
   // (Cornell: 409 vs 262-399 Msamples/s measured), RTAMD_WIDE=1 forces it.
   const char* wenv = std::getenv("RTAMD_WIDE");
   const bool want_wide = wenv ? wenv[0] != '0' : c->rebuilt_bvh;
-  const bool wide = replace && c->d_wnodes && !(p->flags & RT_FLAG_REFERENCE_CULL) && want_wide;
+  // (the full variant has no 4-wide instantiation: its media-free worlds walk the binary tree)
+  const bool wide = replace && c->d_wnodes && !(p->flags & RT_FLAG_REFERENCE_CULL) && want_wide && var != F_ALL;
   const int loop = wide ? 2 : (replace ? 1 : 0);
   // waves per SIMD (measured): spheres 3 (C2 -11 % at 2, -9 % at 4; C5 -15 % at 2); Cornell-like
   // on the replacement loop 3 (C3 380.5 ms vs 453.7 at 2, 428.6 at 4), 1 on the per-sample loop;
-  // full variant (media/frames, per-sample loop) 2 despite 784 B/lane of scratch (C4 at 50 spp:
-  // 35.2 vs 23.4 Msamples/s at 1 wave (457 registers), 9.1 at 3)
-  const int waves = (var == kVarSpheres || (var == kVarCornell && loop)) ? waves_target(3)
-                                                                          : waves_target(var == F_ALL ? 2 : 1);
+  // full variant on the replacement loop 3 (C4 at 100 spp: 90.9 vs 87.5 Msamples/s at 2), on the
+  // per-sample loop 2 despite 784 B/lane of scratch (C4 35.2 vs 23.4 at 1 wave, 9.1 at 3)
+  const int waves = (var == kVarSpheres || loop) ? waves_target(3) : waves_target(var == F_ALL ? 2 : 1);
+  const int side_ints = (var & F_FRAMES) && loop == 1 ? kSideInts : 0;  // Side slots after the stacks
   // LDS-staged kernel when the traversal's node array plus the stacks fit one CU's 160 KiB
   // (RTAMD_LDS=0 disables it for A/B runs).
-  if (!count && !env_off("RTAMD_LDS") && var != F_ALL) {
+  if (!count && !env_off("RTAMD_LDS") && (var != F_ALL || loop)) {
     const int block = waves * 256;
     const int entries = wide ? c->wide_stack_need + 3 : c->stack_need + 2;  // (wide_node writes 3 slots)
     const int items = wide ? c->n_wnodes : c->n_nodes;
     const size_t rec = wide ? sizeof(rt_wnode) : sizeof(rt_node);
-    const size_t bytes = (size_t)items * rec + (size_t)entries * block * sizeof(int);
+    const size_t bytes = (size_t)items * rec + (size_t)(entries + side_ints) * block * sizeof(int);
     if (bytes <= 160 * 1024) {
       const void* fn = philox_kernel(var, loop, true, waves, false);
       HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
@@ -1186,12 +1211,13 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
   c->n_nodes = d->n_nodes;
   // (tie redo walks the caller's tree: size the stacks for both)
   c->stack_need = std::max(v.stack_need[d->world_root], v.stack_need[din->world_root]);
-  c->replace_ok = !(c->features & F_MEDIA);
-  for (const rt_node& x : v.nodes)
-    if (((x.type & RT_TYPE_MASK) == RT_NODE_TRANSLATE || (x.type & RT_TYPE_MASK) == RT_NODE_ROTATE) &&
-        !(x.type & RT_CHAIN_PRIM))
-      c->replace_ok = false;
-  if (c->replace_ok) {  // 4-wide fp32-box tree over the same world tree (unflagged node copy)
+  // The replacement loop takes every world whose frames nest at most RT_MAX_FRAMES deep (its Side
+  // slots); worlds with media or frames walk the caller's tree in the reference's order.
+  const bool frames = v.frame_depth[d->world_root] > 0;
+  c->replace_ok = v.frame_depth[d->world_root] <= RT_MAX_FRAMES;
+  S.ref_walk = (c->features & F_MEDIA) || frames;
+  if (frames) c->features |= F_FRAMES;
+  if (c->replace_ok && !S.ref_walk) {  // 4-wide fp32-box tree over the same world tree (unflagged node copy)
     std::vector<rt_wnode> wide;
     int need = 0;
     if (rt::build_wide_bvh(nodes, d->world_root, wide, &need) && need + 3 <= RT_WSTACK &&

@@ -12,7 +12,8 @@ enum : unsigned {
   F_MEDIA = 8u,   // ConstantMedium (+ Isotropic)
   F_LIGHTS = 16u, // a lights tree (Lambertian light sampling / pdf)
   F_TEX = 32u,    // Checker / Perlin / Image textures (and sphere u, v)
-  F_ALL = 63u,
+  F_FRAMES = 512u,  // instance frames (Translate/Rotate over a BVH) in the resumable walk
+  F_ALL = 63u | 512u,
   F_UV = 64u,     // always compute sphere (u, v) (debug queries)
   F_COUNT = 128u, // counting build: per-lane work counters (DESIGN.md "Roofline")
   F_WIDE = 256u   // resumable walk over the 4-wide fp32-box tree (rt_wide.h) instead of the binary one
@@ -506,6 +507,34 @@ __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr
 }
 
 // ------------------------------------------------------------------ resumable traversal
+// Per-lane LDS slots of the resumable walk over worlds with instance frames (`stride` ints apart):
+// the world ray (restored when the last frame closes), the ids of the open frames, and of the
+// frames around the best hit (Trav::best_level of them).
+constexpr int kSideInts = 14 + 2 * RT_MAX_FRAMES;
+struct Side {
+  int* p;
+  int stride;
+  __device__ __forceinline__ void put_d(int i, double x) {
+    const long long b = __double_as_longlong(x);
+    p[(2 * i) * stride] = (int)(b & 0xffffffff);
+    p[(2 * i + 1) * stride] = (int)(b >> 32);
+  }
+  __device__ __forceinline__ double get_d(int i) const {
+    return __hiloint2double(p[(2 * i + 1) * stride], p[(2 * i) * stride]);
+  }
+  __device__ __forceinline__ void put_ray(const Ray& r) {
+    put_d(0, r.o.x), put_d(1, r.o.y), put_d(2, r.o.z), put_d(3, r.d.x), put_d(4, r.d.y), put_d(5, r.d.z);
+    put_d(6, r.tm);
+  }
+  __device__ __forceinline__ Ray get_ray() const {
+    return Ray{v3(get_d(0), get_d(1), get_d(2)), v3(get_d(3), get_d(4), get_d(5)), get_d(6)};
+  }
+  __device__ __forceinline__ int& frame(int i) { return p[(14 + i) * stride]; }
+  __device__ __forceinline__ int& best(int i) { return p[(14 + RT_MAX_FRAMES + i) * stride]; }
+  __device__ __forceinline__ int best(int i) const { return p[(14 + RT_MAX_FRAMES + i) * stride]; }
+};
+constexpr int kSubChain = -1, kSubMedium = -2;  // Trav::best_sub of a chain / ConstantMedium hit
+
 // The same depth-first closest-hit walk as `traverse`, one node per call, with its state kept in
 // registers between calls (stack in LDS), for worlds without ConstantMedium and without instance
 // frames (instances over primitive chains are leaves here). Lets a wave keep every lane busy:
@@ -517,6 +546,8 @@ struct Trav {
   double best_tmax;   // chain hits: the bound in force when the best hit was found
   int node, sp, best_node, best_sub;
   int pend;           // F_WIDE: a postponed leaf (flat node id), -1 = none
+  int level;          // F_INST: open instance frames (their ids in the lane's Side slots)
+  int best_level;     // F_INST: frames around the best hit (copied to Side::best)
   bool tie;           // a second leaf hit at exactly `closest`: the walk is redone with `ref`
   bool ref;           // the reference's own walk: caller's tree, left first, bound = closest
   // F_WIDE: the ray in fp32 for the conservative child-box test (wide_keys2)
@@ -545,6 +576,8 @@ __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r, int root, doub
   t.best_node = -1;
   t.best_sub = 0;
   t.pend = -1;
+  t.level = 0;
+  t.best_level = 0;
   t.tie = false;
   t.ref = false;
   if constexpr ((F & F_WIDE) != 0) {
@@ -591,6 +624,8 @@ __device__ __forceinline__ void trav_restart_ref(Trav& t, int root, double t_max
   t.best_node = -1;
   t.best_sub = 0;
   t.pend = -1;
+  t.level = 0;
+  t.best_level = 0;
   t.tie = false;
   t.ref = true;
 }
@@ -603,31 +638,42 @@ __device__ __forceinline__ void trav_restart_ref(Trav& t, int root, double t_max
 // Exact ties need two surfaces through one point on the ray (e.g. the book-one glass sphere
 // resting on the ground at (0,0,0)); they are rare, so the redo costs nothing measurable.
 template <unsigned F>
-__device__ __forceinline__ void trav_take(Trav& t, double x, int id, int sub) {
+__device__ __forceinline__ void trav_take(Trav& t, double x, int id, int sub, Side& side) {
   if (t.ref || x < t.closest) {  // (ref: every accepted hit replaces, as hit BVHNode prefers the right one)
     t.best_tmax = t.closest_up;
     t.closest = x;
     t.closest_up = t.ref ? x : nextafter(x, INFINITY);
     t.best_node = id;
     t.best_sub = sub;
+    if constexpr ((F & F_FRAMES) != 0) {
+      t.best_level = t.level;
+      for (int k = 0; k < t.level; ++k) side.best(k) = side.frame(k);
+    }
     if constexpr ((F & F_WIDE) != 0) t.tmax32 = f32_upper(x);
   } else if (x == t.closest && id != t.best_node) {  // (the same leaf twice is no tie)
     t.tie = true;
   }
 }
-template <unsigned F>
-__device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, int id, double t_min, Cnt& cnt) {
+// A leaf: a primitive, an instance chain ending in one (its t only: the record is built once, in
+// trav_finish), or a ConstantMedium (ref walks only: its one draw happens here, in the
+// reference's order and under its bound, Lib.hs:1053-1080).
+template <unsigned F, class R>
+__device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, int id, double t_min, Cnt& cnt, R& g, Side& side) {
   const rt_node* n = &S.nodes[id];
   const int type = n->type & RT_TYPE_MASK;
   if ((F & F_INST) && (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE)) {
     if constexpr ((F & F_COUNT) != 0) ++cnt.other;
+    double tt;
+    if (chain_t<F>(S, id, plain(t.ray), t_min, t.closest_up, tt)) trav_take<F>(t, tt, id, kSubChain, side);
+  } else if ((F & F_MEDIA) && type == RT_NODE_CONSTANT_MEDIUM) {
+    if constexpr ((F & F_COUNT) != 0) ++cnt.other;
     Hit h;
-    if (chain_hit<F>(S, id, plain(t.ray), t_min, t.closest_up, h)) trav_take<F>(t, h.t, id, -1);
+    if (medium_hit<F>(S, n, plain(t.ray), t_min, t.closest, g, h)) trav_take<F>(t, h.t, id, kSubMedium, side);
   } else {
     if constexpr ((F & F_COUNT) != 0) ++cnt.prim;
     double tt;
     int sub;
-    if (prim_t<F>(S, n, t.ray, t_min, t.closest_up, tt, sub)) trav_take<F>(t, tt, id, sub);
+    if (prim_t<F>(S, n, t.ray, t_min, t.closest_up, tt, sub)) trav_take<F>(t, tt, id, sub, side);
   }
 }
 
@@ -705,10 +751,13 @@ __device__ __forceinline__ bool wide_node(const Scene& S, Trav& t, int* stk, int
   return n_hit != 0;
 }
 
-// Visit one node; false once the walk is over.
-template <unsigned F>
+// Visit one node; false once the walk is over. The binary walk also opens instance frames
+// (Translate/Rotate over a BVH, Lib.hs:1029-1052): a tagged stack entry, the frame's id in the
+// lane's Side slots, and the child's ray in Trav::ray; when the entry is popped the parent's ray is
+// rebuilt from the world ray through the frames still open (the same operations as on entry).
+template <unsigned F, class R>
 __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min, int* stk, int stride, bool joint,
-                                          Cnt& cnt) {
+                                          Cnt& cnt, R& g, Side& side) {
   bool wide = false;
   if constexpr ((F & F_WIDE) != 0) wide = !t.ref;
   if (wide) {
@@ -716,27 +765,47 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
       if constexpr ((F & F_COUNT) != 0) ++cnt.wide;
       if (wide_node(S, t, stk, stride)) return true;
     } else {
-      trav_leaf<F>(S, t, ~t.node, t_min, cnt);
+      trav_leaf<F>(S, t, ~t.node, t_min, cnt, g, side);
     }
-  } else {
-    const rt_node* n = &S.nodes[t.node];
-    const int type = n->type & RT_TYPE_MASK;
-    if (type == RT_NODE_BVH) {
-      if constexpr ((F & F_COUNT) != 0) ++cnt.box;
-      if (box_hit(n->f, t.ray, t_min, t.closest_up, joint)) {
-        const int c = n->c;
-        const bool flip = (c & RT_BVH_ORDERED) && comp(t.ray.d, c & 3) < 0;
-        stk[(t.sp++) * stride] = flip ? n->a : n->b;
-        t.node = flip ? n->b : n->a;
-        return true;
-      }
-    } else {
-      trav_leaf<F>(S, t, t.node, t_min, cnt);
-    }
+    if (t.sp == 0) return false;
+    t.node = stk[(--t.sp) * stride];
+    return true;
   }
-  if (t.sp == 0) return false;
-  t.node = stk[(--t.sp) * stride];
-  return true;
+  const rt_node* n = &S.nodes[t.node];
+  const int tf = n->type;
+  const int type = tf & RT_TYPE_MASK;
+  if (type == RT_NODE_BVH) {
+    if constexpr ((F & F_COUNT) != 0) ++cnt.box;
+    if (box_hit(n->f, t.ray, t_min, t.closest_up, joint)) {
+      const int c = n->c;
+      const bool flip = (c & RT_BVH_ORDERED) && comp(t.ray.d, c & 3) < 0;
+      stk[(t.sp++) * stride] = flip ? n->a : n->b;
+      t.node = flip ? n->b : n->a;
+      return true;
+    }
+  } else if ((F & F_FRAMES) && (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE) && !(tf & RT_CHAIN_PRIM)) {
+    if constexpr ((F & F_COUNT) != 0) ++cnt.other;
+    if (t.level == 0) side.put_ray(plain(t.ray));
+    side.frame(t.level++) = t.node;
+    stk[(t.sp++) * stride] = RT_FRAME | t.node;
+    t.ray = prep(enter_instance(n, plain(t.ray)));
+    t.node = n->a;
+    return true;
+  } else {
+    trav_leaf<F>(S, t, t.node, t_min, cnt, g, side);
+  }
+  for (;;) {
+    if (t.sp == 0) return false;
+    const int e = stk[(--t.sp) * stride];
+    if (!(F & F_FRAMES) || !(e & RT_FRAME)) {
+      t.node = e;
+      return true;
+    }
+    --t.level;  // a frame closes
+    Ray pr = side.get_ray();
+    for (int k = 0; k < t.level; ++k) pr = enter_instance(&S.nodes[side.frame(k)], pr);
+    t.ray = prep(pr);
+  }
 }
 
 // ---- the 4-wide walk with postponed leaves (Aila & Laine's while-while, one postponed slot)
@@ -763,10 +832,11 @@ __device__ __forceinline__ void wide_inner(const Scene& S, Trav& t, int* stk, in
   if (!wide_node(S, t, stk, stride)) t.node = trav_pop(t, stk, stride);
   trav_postpone(t, stk, stride);
 }
-template <unsigned F>
-__device__ __forceinline__ void wide_leaf(const Scene& S, Trav& t, double t_min, int* stk, int stride, Cnt& cnt) {
+template <unsigned F, class R>
+__device__ __forceinline__ void wide_leaf(const Scene& S, Trav& t, double t_min, int* stk, int stride, Cnt& cnt, R& g,
+                                          Side& side) {
   if (t.pend >= 0) {
-    trav_leaf<F>(S, t, t.pend, t_min, cnt);
+    trav_leaf<F>(S, t, t.pend, t_min, cnt, g, side);
     t.pend = -1;
   }
   trav_postpone(t, stk, stride);
@@ -775,14 +845,14 @@ __device__ __forceinline__ void wide_leaf(const Scene& S, Trav& t, double t_min,
 // Step the wave's walking lanes until at most `stop` of them still walk (`walking` goes false when
 // a lane's walk is over). Binary walks: one node per lane per step. 4-wide walks: wide-node steps
 // until at most `leaf_stop` walking lanes still look for their first leaf, then one leaf step.
-template <unsigned F>
+template <unsigned F, class R>
 __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walking, double t_min, int* stk, int stride,
-                                           bool joint, int stop, int leaf_stop, Cnt& cnt) {
+                                           bool joint, int stop, int leaf_stop, Cnt& cnt, R& g, Side& side) {
   if constexpr ((F & F_WIDE) == 0) {
     (void)leaf_stop;
     for (;;) {
       if (__popcll(__ballot(walking)) <= stop) break;
-      if (walking) walking = trav_step<F>(S, t, t_min, stk, stride, joint, cnt);
+      if (walking) walking = trav_step<F>(S, t, t_min, stk, stride, joint, cnt, g, side);
     }
   } else {
     for (;;) {
@@ -794,7 +864,7 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
       if (__popcll(__ballot(seeking)) > leaf_stop || __ballot(holding) == 0) {
         if constexpr ((F & F_COUNT) != 0) ++cnt.islot;
         if (walking && t.ref) {
-          walking = trav_step<F>(S, t, t_min, stk, stride, joint, cnt);
+          walking = trav_step<F>(S, t, t_min, stk, stride, joint, cnt, g, side);
         } else if (walking && t.node >= 0) {
           wide_inner<F>(S, t, stk, stride, cnt);
           walking = t.node != kNone || t.pend >= 0;
@@ -802,7 +872,7 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
       } else {
         if constexpr ((F & F_COUNT) != 0) ++cnt.lslot;
         if (holding) {
-          wide_leaf<F>(S, t, t_min, stk, stride, cnt);
+          wide_leaf<F>(S, t, t_min, stk, stride, cnt, g, side);
           walking = t.node != kNone || t.pend >= 0;
         }
       }
@@ -811,15 +881,47 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
 }
 
 // The closest hit's record, built once from the same ray with the same operations (a chain
-// hit is re-run under the bound that was in force when it was found). Callers check `tie`
-// first and re-walk with trav_restart_ref.
+// hit is re-run under the bound that was in force when it was found; a medium's record is its
+// t, the point on the ray, normal (1,0,0), u = v = 0, front face, Lib.hs:1074-1080). A hit inside
+// instance frames is recorded in the innermost frame's ray, then each frame's rewrite is applied
+// from the innermost outwards with the ray its child saw (as `traverse` does when frames close).
+// `r` is the world ray. Callers check `tie` first and re-walk with trav_restart_ref.
 template <unsigned F>
-__device__ __forceinline__ bool trav_finish(const Scene& S, const Trav& t, const Ray& r, double t_min, Hit& h) {
-  if (t.best_node < 0) return false;
+__device__ __forceinline__ bool leaf_record(const Scene& S, const Trav& t, const Ray& r, double t_min, Hit& h) {
   if constexpr ((F & F_INST) != 0)
-    if (t.best_sub < 0) return chain_hit<F>(S, t.best_node, r, t_min, t.best_tmax, h);
+    if (t.best_sub == kSubChain) return chain_hit<F>(S, t.best_node, r, t_min, t.best_tmax, h);
+  if constexpr ((F & F_MEDIA) != 0)
+    if (t.best_sub == kSubMedium) {
+      h.t = t.closest;
+      h.p = at(r, t.closest);
+      h.n = v3(1, 0, 0);
+      h.u = 0;
+      h.v = 0;
+      h.ff = 1;
+      h.mat = S.nodes[t.best_node].b;
+      return true;
+    }
   prim_record<F>(S, &S.nodes[t.best_node], t.best_sub, r, t.closest, h);
   return true;
+}
+template <unsigned F>
+__device__ __forceinline__ bool trav_finish(const Scene& S, const Trav& t, const Ray& r, double t_min, Hit& h,
+                                            const Side& side) {
+  if (t.best_node < 0) return false;
+  if constexpr ((F & F_FRAMES) != 0) {
+    if (t.best_level > 0) {
+      Ray fr = r;
+      for (int k = 0; k < t.best_level; ++k) fr = enter_instance(&S.nodes[side.best(k)], fr);
+      leaf_record<F>(S, t, fr, t_min, h);
+      for (int lv = t.best_level - 1; lv >= 0; --lv) {
+        Ray rc = r;  // the ray frame lv's child saw
+        for (int k = 0; k <= lv; ++k) rc = enter_instance(&S.nodes[side.best(k)], rc);
+        exit_instance(&S.nodes[side.best(lv)], rc, h);
+      }
+      return true;
+    }
+  }
+  return leaf_record<F>(S, t, r, t_min, h);
 }
 
 // ------------------------------------------------------------------ lights (Lib.hs:662-724)

@@ -104,12 +104,14 @@ def _ulp_close(a, b, ulps):
     return np.abs(a - b) <= ulps * np.spacing(np.maximum(np.abs(a), np.abs(b)))
 
 
-@pytest.mark.parametrize("flags", [0, rtamd.RT_FLAG_REFERENCE_CULL])
+@pytest.mark.parametrize("flags", [0, rtamd.RT_FLAG_REFERENCE_CULL, rtamd.RT_DEBUG_RESUMABLE])
 @pytest.mark.parametrize("name", ["random_book_one", "cornell", "next_week_final", "cornell_smoke"])
 def test_closest_hits_bit_exact(gpu_ctx, name, flags):
-    """hit over the whole world DAG. Surface hits: t, p, normal, frontFace, material bit-identical
-    (u, v of spheres go through atan/asin: within 2 ulps). Medium hits: t through `log` (OCML vs
-    glibc, <= 1 ulp apart), so t and p within 4 ulps, the rest exact."""
+    """hit over the whole world DAG, by the recursive walk (flags 0 / reference cull) and by the
+    render loop's resumable walk (media and instance frames walked in the reference's order,
+    records rebuilt through the frames at the end). Surface hits: t, p, normal, frontFace,
+    material bit-identical (u, v of spheres go through atan/asin: within 2 ulps). Medium hits: t
+    through `log` (OCML vs glibc, <= 1 ulp apart), so t and p within 4 ulps, the rest exact."""
     earth = np.load(_earth_path())["rgb"] if name == "next_week_final" else None
     sc, _ = _scene(name, earth=earth)
     gpu_ctx.upload(sc)
@@ -204,11 +206,14 @@ def test_resumable_walks_closest_hits(gpu_ctx, name, walk):
     assert np.all(du <= 2e-15), f"u/v max |d| {du.max():.3g}"
 
 
-@pytest.mark.parametrize("name,cam", [("random_book_one", "random_scene"), ("cornell", "cornell")])
+@pytest.mark.parametrize("name,cam", [("random_book_one", "random_scene"), ("cornell", "cornell"),
+                                      ("next_week_final", "next_week"), ("cornell_smoke", "cornell")])
 def test_walks_output_identical(gpu_ctx, name, cam, monkeypatch):
     """Full tier-B images: 4-wide walk == binary replacement walk == one-sample-per-lane loop,
-    byte for byte and in the linear averages (the walks differ only in which boxes they cull)."""
-    sc, _ = _scene(name)
+    byte for byte and in the linear averages (the walks differ only in which boxes they cull; worlds
+    with media or frames take the reference's own order in both loops)."""
+    earth = np.load(_earth_path())["rgb"] if name == "next_week_final" else None
+    sc, _ = _scene(name, earth=earth)
     c = rtamd.camera(cam, 160, 96)
     gpu_ctx.upload(sc)
     p = rtamd.make_params(160, 96, 4, 50, rtamd.RT_RNG_PHILOX, seed=5)
