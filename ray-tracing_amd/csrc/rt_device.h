@@ -128,6 +128,7 @@ struct DMat {
 struct Scene {
   const rt_node* nodes;
   const rt_wnode* wnodes;  // 4-wide world tree (F_WIDE kernels); null when not built
+  const rt_node* leaves;   // its leaf table: referenced leaves (c = flat node id), LDS or global
   const DMat* mats;
   const rt_texture* texs;
   const rt_perlin* perlins;

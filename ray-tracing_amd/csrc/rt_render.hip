@@ -506,7 +506,8 @@ __global__ void __launch_bounds__(RT_BLOCK, WAVES) render_philox2(RenderArgs A) 
 // flat nodes) and the per-lane stacks live in the CU's LDS; leaves are read from global memory
 // under F_WIDE.
 template <unsigned F, int WAVES>
-__global__ void __launch_bounds__(WAVES * 256, WAVES) render_philox2_lds(RenderArgs A, int n_nodes, int stack_entries) {
+__global__ void __launch_bounds__(WAVES * 256, WAVES)
+    render_philox2_lds(RenderArgs A, int n_nodes, int stack_entries, int n_leaves) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   constexpr int rec = (F & F_WIDE) ? (int)sizeof(rt_wnode) : (int)sizeof(rt_node);
   {
@@ -515,12 +516,18 @@ __global__ void __launch_bounds__(WAVES * 256, WAVES) render_philox2_lds(RenderA
     uint4* dst = reinterpret_cast<uint4*>(lds);
     const int n16 = n_nodes * (rec / 16);
     for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+    // F_WIDE: the leaf table too, when it fits (n_leaves > 0)
+    const uint4* lsrc = reinterpret_cast<const uint4*>(A.S.leaves);
+    uint4* ldst = reinterpret_cast<uint4*>(lds + (size_t)n_nodes * rec);
+    const int l16 = n_leaves * (int)(sizeof(rt_node) / 16);
+    for (int i = threadIdx.x; i < l16; i += blockDim.x) ldst[i] = lsrc[i];
   }
   __syncthreads();
   Scene S = A.S;
   if constexpr ((F & F_WIDE) != 0) S.wnodes = reinterpret_cast<const rt_wnode*>(lds);
   else S.nodes = reinterpret_cast<const rt_node*>(lds);
-  int* stk = reinterpret_cast<int*>(lds + (size_t)n_nodes * rec) + threadIdx.x;
+  if (n_leaves > 0) S.leaves = reinterpret_cast<const rt_node*>(lds + (size_t)n_nodes * rec);
+  int* stk = reinterpret_cast<int*>(lds + (size_t)n_nodes * rec + (size_t)n_leaves * sizeof(rt_node)) + threadIdx.x;
   // (the host sizes the dynamic LDS for stack_entries stack ints + kSideInts Side ints per lane
   // when F has F_FRAMES)
   philox_loop2<F>(A, S, stk, WAVES * 256, stk + stack_entries * WAVES * 256);
@@ -683,6 +690,8 @@ struct rt_ctx {
   int n_nodes = 0;
   int stack_need = 0;  // deepest traversal stack the world tree needs (entries)
   rt_wnode* d_wnodes = nullptr;  // 4-wide world tree (replace_ok worlds with a BVH root)
+  rt_node* d_leaves = nullptr;   // its leaf table (Scene::leaves)
+  int n_leaves = 0;
   int n_wnodes = 0;
   int wide_stack_need = 0;
   bool rebuilt_bvh = false;
@@ -723,7 +732,10 @@ void free_scene(rt_ctx* c) {
   (void)hipFree(c->d_images);
   (void)hipFree(c->d_pool);
   (void)hipFree(c->d_wnodes);
+  (void)hipFree(c->d_leaves);
   c->d_wnodes = nullptr;
+  c->d_leaves = nullptr;
+  c->n_leaves = 0;
   c->n_wnodes = 0;
   c->d_nodes = nullptr;
   c->d_mats = nullptr;
@@ -1057,12 +1069,16 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
     const int entries = wide ? c->wide_stack_need + 3 : c->stack_need + 2;  // (wide_node writes 3 slots)
     const int items = wide ? c->n_wnodes : c->n_nodes;
     const size_t rec = wide ? sizeof(rt_wnode) : sizeof(rt_node);
-    const size_t bytes = (size_t)items * rec + (size_t)(entries + side_ints) * block * sizeof(int);
+    size_t bytes = (size_t)items * rec + (size_t)(entries + side_ints) * block * sizeof(int);
+    // the wide walk's leaf table joins the nodes in LDS when it fits as well (RTAMD_LEAF_LDS=0: never)
+    int n_leaves = wide && !env_off("RTAMD_LEAF_LDS") ? c->n_leaves : 0;
+    if (bytes + (size_t)n_leaves * sizeof(rt_node) > 160 * 1024) n_leaves = 0;
+    bytes += (size_t)n_leaves * sizeof(rt_node);
     if (bytes <= 160 * 1024) {
       const void* fn = philox_kernel(var, loop, true, waves, false);
       HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
       int n_items = items;
-      void* args[] = {&A, &n_items, (void*)&entries};
+      void* args[] = {&A, &n_items, (void*)&entries, &n_leaves};
       HIPCHK(hipEventRecord(c->ev0, st));
       HIPCHK(hipLaunchKernel(fn, dim3(c->cu_count), dim3(block), args, bytes, st));
       HIPCHK(hipEventRecord(c->ev1, st));
@@ -1222,16 +1238,35 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
     int need = 0;
     if (rt::build_wide_bvh(nodes, d->world_root, wide, &need) && need + 3 <= RT_WSTACK &&
         (size_t)wide.size() < (size_t)INT32_MAX / 2) {
-      if ((rc = upload(&c->d_wnodes, wide.data(), wide.size()))) {
+      // The walk's leaf table: the leaves the wide tree references, each copied once (a moving
+      // sphere with its EXT record), with `c` = the flat node id; leaf references ~id become ~slot.
+      std::vector<rt_node> leaves;
+      std::vector<int> slot(v.nodes.size(), -1);
+      for (rt_wnode& w : wide)
+        for (int k = 0; k < RT_WIDE; ++k) {
+          if (w.child[k] >= 0) continue;
+          const int id = ~w.child[k];
+          if (slot[id] < 0) {
+            slot[id] = (int)leaves.size();
+            leaves.push_back(v.nodes[id]);
+            leaves.back().c = id;
+            if ((v.nodes[id].type & RT_TYPE_MASK) == RT_NODE_MOVING_SPHERE) leaves.push_back(v.nodes[id + 1]);
+          }
+          w.child[k] = ~slot[id];
+        }
+      if ((rc = upload(&c->d_wnodes, wide.data(), wide.size())) ||
+          (rc = upload(&c->d_leaves, leaves.data(), leaves.size()))) {
         free_scene(c);
         return rc;
       }
+      c->n_leaves = (int)leaves.size();
+      S.leaves = c->d_leaves;
       c->n_wnodes = (int)wide.size();
       c->wide_stack_need = std::max(need, v.stack_need[din->world_root]);
       S.wnodes = c->d_wnodes;
     }
   }
-  if (!c->d_wnodes) S.wnodes = nullptr;
+  if (!c->d_wnodes) S.wnodes = nullptr, S.leaves = nullptr;
   c->has_scene = true;
   return RT_OK;
 }

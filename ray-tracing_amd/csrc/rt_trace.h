@@ -658,8 +658,8 @@ __device__ __forceinline__ void trav_take(Trav& t, double x, int id, int sub, Si
 // trav_finish), or a ConstantMedium (ref walks only: its one draw happens here, in the
 // reference's order and under its bound, Lib.hs:1053-1080).
 template <unsigned F, class R>
-__device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, int id, double t_min, Cnt& cnt, R& g, Side& side) {
-  const rt_node* n = &S.nodes[id];
+__device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, const rt_node* n, int id, double t_min, Cnt& cnt,
+                                          R& g, Side& side) {
   const int type = n->type & RT_TYPE_MASK;
   if ((F & F_INST) && (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE)) {
     if constexpr ((F & F_COUNT) != 0) ++cnt.other;
@@ -765,7 +765,8 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
       if constexpr ((F & F_COUNT) != 0) ++cnt.wide;
       if (wide_node(S, t, stk, stride)) return true;
     } else {
-      trav_leaf<F>(S, t, ~t.node, t_min, cnt, g, side);
+      const rt_node* n = &S.leaves[~t.node];
+      trav_leaf<F>(S, t, n, n->c, t_min, cnt, g, side);
     }
     if (t.sp == 0) return false;
     t.node = stk[(--t.sp) * stride];
@@ -792,7 +793,7 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
     t.node = n->a;
     return true;
   } else {
-    trav_leaf<F>(S, t, t.node, t_min, cnt, g, side);
+    trav_leaf<F>(S, t, n, t.node, t_min, cnt, g, side);
   }
   for (;;) {
     if (t.sp == 0) return false;
@@ -836,7 +837,8 @@ template <unsigned F, class R>
 __device__ __forceinline__ void wide_leaf(const Scene& S, Trav& t, double t_min, int* stk, int stride, Cnt& cnt, R& g,
                                           Side& side) {
   if (t.pend >= 0) {
-    trav_leaf<F>(S, t, t.pend, t_min, cnt, g, side);
+    const rt_node* n = &S.leaves[t.pend];  // (pend holds the leaf table slot)
+    trav_leaf<F>(S, t, n, n->c, t_min, cnt, g, side);
     t.pend = -1;
   }
   trav_postpone(t, stk, stride);
