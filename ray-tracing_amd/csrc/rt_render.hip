@@ -47,15 +47,35 @@ __device__ __forceinline__ unsigned long long stamp() {
   return t;
 }
 
+// Unsigned 32-bit division by an invariant divisor d >= 1 (Granlund & Montgomery): with
+// l = ceil(log2 d) and m = floor(2^32 (2^l - d) / d) + 1, n / d = (t + ((n - t) >> s1)) >> s2 for
+// every 32-bit n, t = umulhi(m, n), s1 = min(l, 1), s2 = max(l - 1, 0). One multiply and a few
+// shifts instead of the software division a `/` on the device becomes.
+struct UDiv {
+  uint32_t m;
+  int s1, s2;
+};
+inline UDiv make_udiv(uint32_t d) {
+  int l = 0;
+  while ((1ull << l) < d) ++l;
+  const uint64_t m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
+  return UDiv{(uint32_t)m, l < 1 ? l : 1, l > 1 ? l - 1 : 0};
+}
+__device__ __forceinline__ uint32_t udiv(uint32_t n, UDiv d) {
+  const uint32_t t = __umulhi(d.m, n);
+  return (t + ((n - t) >> d.s1)) >> d.s2;
+}
+
 struct RenderArgs {
   Scene S;
   rt_camera cam;
   int W, H, spp, max_depth;
   uint32_t flags;
   int tile, tiles_x, tiles_total, shard_rank, shard_count;
-  long long work_total;  // work-items of this shard: slab pixels x sample chunks
+  long long work_total;  // work-items of this shard: slab pixels x sample chunks (< 2^32)
   long long slab;        // slab pixels of this shard
   int chunk, chunks;     // tier B: samples per chunk (rt_sample_chunk) and chunks per pixel
+  UDiv div_tp, div_tile, div_tiles_x, div_bpr;  // by tile*tile, tile*tile*chunks, tiles_x, tile/8
   double* partial;       // tier B: chunk sums, [chunk][slab pixel][3]
   uint64_t seed;
   unsigned long long* counter;
@@ -67,18 +87,19 @@ struct RenderArgs {
   uint64_t* gens;  // tier A: per-column (seed, gamma), updated in place
 };
 
-// Slab pixel index -> image pixel (tile-major, 8x8 blocks inside a tile).
-__device__ __forceinline__ bool work_pixel(const RenderArgs& A, long long w, int& px, int& row) {
-  const long long tp = (long long)A.tile * A.tile;
-  const long long lt = w / tp;
-  const int within = (int)(w - lt * tp);
-  const long long gt = (long long)A.shard_rank + lt * A.shard_count;
+// Slab pixel index -> image pixel (tile-major, 8x8 blocks inside a tile). Slab indices are < 2^32
+// (launch_philox checks).
+__device__ __forceinline__ bool work_pixel(const RenderArgs& A, uint32_t w, int& px, int& row) {
+  const uint32_t tp = (uint32_t)(A.tile * A.tile);
+  const uint32_t lt = udiv(w, A.div_tp);
+  const uint32_t within = w - lt * tp;
+  const long long gt = (long long)A.shard_rank + (long long)lt * A.shard_count;
   if (gt >= A.tiles_total) return false;
-  const int tx = (int)(gt % A.tiles_x), ty = (int)(gt / A.tiles_x);
-  const int bpr = A.tile >> 3;
-  const int blk = within >> 6, l = within & 63;
-  px = tx * A.tile + (blk % bpr) * 8 + (l & 7);
-  row = ty * A.tile + (blk / bpr) * 8 + (l >> 3);
+  const uint32_t ty = udiv((uint32_t)gt, A.div_tiles_x), tx = (uint32_t)gt - ty * (uint32_t)A.tiles_x;
+  const uint32_t blk = within >> 6, l = within & 63;
+  const uint32_t by = udiv(blk, A.div_bpr), bx = blk - by * (uint32_t)(A.tile >> 3);
+  px = (int)(tx * A.tile + bx * 8 + (l & 7));
+  row = (int)(ty * A.tile + by * 8 + (l >> 3));
   return px < A.W && row < A.H;
 }
 
@@ -86,16 +107,15 @@ __device__ __forceinline__ bool work_pixel(const RenderArgs& A, long long w, int
 // tile, so a wave's 64 consecutive items are one 8x8 pixel block at one chunk (coherent rays).
 // Returns false for pixels outside the image; else the sample range [s0, s1) and the chunk
 // sum's slot in `partial`.
-__device__ __forceinline__ bool work_item(const RenderArgs& A, long long wi, int& px, int& row, int& s0, int& s1,
+__device__ __forceinline__ bool work_item(const RenderArgs& A, uint32_t wi, int& px, int& row, int& s0, int& s1,
                                           long long& slot) {
-  const long long tp = (long long)A.tile * A.tile;
-  const long long per_tile = tp * A.chunks;
-  const long long lt = wi / per_tile;
-  const long long rem = wi - lt * per_tile;
-  const int k = (int)(rem / tp);
-  const long long idx = lt * tp + (rem - (long long)k * tp);
+  const uint32_t tp = (uint32_t)(A.tile * A.tile);
+  const uint32_t lt = udiv(wi, A.div_tile);  // by tp * chunks
+  const uint32_t rem = wi - lt * tp * (uint32_t)A.chunks;
+  const uint32_t k = udiv(rem, A.div_tp);
+  const uint32_t idx = lt * tp + (rem - k * tp);
   if (!work_pixel(A, idx, px, row)) return false;
-  s0 = k * A.chunk;
+  s0 = (int)k * A.chunk;
   s1 = min(A.spp, s0 + A.chunk);
   slot = (long long)k * A.slab + idx;
   return s0 < s1;
@@ -250,7 +270,7 @@ __device__ __forceinline__ void philox_loop(const RenderArgs& A, const Scene& S,
         const long long wi = (long long)(base + __popcll(mask & lanes_below));
         if (wi >= A.work_total) {
           done = true;
-        } else if (work_item(A, wi, px, row, s, s_end, w)) {
+        } else if (work_item(A, (uint32_t)wi, px, row, s, s_end, w)) {
           sum = v3(0, 0, 0);
           path = false;
         } else {
@@ -426,7 +446,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
           const long long wi = (long long)(base + __popcll(mask & lanes_below));
           if (wi >= A.work_total) {
             done = true;
-          } else if (work_item(A, wi, px, row, s, s_end, w)) {
+          } else if (work_item(A, (uint32_t)wi, px, row, s, s_end, w)) {
             sum = v3(0, 0, 0);
           } else {
             w = -1;
@@ -538,7 +558,7 @@ __global__ void __launch_bounds__(256) combine_chunks(RenderArgs A) {
   const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
   if (idx >= A.slab) return;
   int px, row;
-  if (!work_pixel(A, idx, px, row)) return;  // outside the image: never assembled
+  if (!work_pixel(A, (uint32_t)idx, px, row)) return;  // outside the image: never assembled
   V3 acc = v3(0, 0, 0);
   for (int k = 0; k < A.chunks; ++k) {
     const double* q = A.partial + ((long long)k * A.slab + idx) * 3;
@@ -1016,6 +1036,11 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   A.chunk = rt_sample_chunk(p->spp);
   A.chunks = (p->spp + A.chunk - 1) / A.chunk;
   A.work_total = slab * A.chunks;
+  if (A.work_total >= (1ll << 32)) return invalid("image too large: more than 2^32 work-items per shard");
+  A.div_tp = make_udiv((uint32_t)(A.tile * A.tile));
+  A.div_tile = make_udiv((uint32_t)(A.tile * A.tile * A.chunks));
+  A.div_tiles_x = make_udiv((uint32_t)A.tiles_x);
+  A.div_bpr = make_udiv((uint32_t)(A.tile >> 3));
   A.seed = p->seed;
   A.counter = c->d_counter;
   A.work = d_work;

@@ -57,7 +57,7 @@ def test_book_one_tier_b(gpu_ctx):
 
 @pytest.mark.parametrize("spp", [33, 70])
 def test_tier_b_sample_chunks(gpu_ctx, spp):
-    """spp > RT_SAMPLE_CHUNKS: a pixel's samples are summed per chunk (rt_sample_chunk), chunk sums
+    """spp > RT_CHUNK_SAMPLES: a pixel's samples are summed per chunk (rt_sample_chunk), chunk sums
     in chunk order — the device's work-items, combined by `combine_chunks` — exactly as the oracle."""
     sc, _ = _scene("random_book_one")
     cam = rtamd.camera("random_scene", 32, 24)
