@@ -377,7 +377,8 @@ int rt_debug_closest_hits(rt_ctx* ctx, const double* rays, int n, double tmin, d
 /*
  * Debug / numerics probe: out[i] = op(x[i], y[i]) evaluated on the device.
  * ops: 0 x/y (IEEE), 1 div_exact(x, y) (reciprocal + Markstein), 2 sqrt x, 3 sin x, 4 cos x,
- * 5 atan x, 6 asin x, 7 log x, 8 pow(x, y), 9 GHC atan2(x, y), 10 tan x.
+ * 5 atan x, 6 asin x, 7 log x, 8 pow(x, y), 9 GHC atan2(x, y), 10 tan x, 11 the render path's
+ * x ** 5 (schlick; double-double, correctly rounded).
  */
 int rt_debug_math(rt_ctx* ctx, int op, const double* x, const double* y, int n, double* out);
 

@@ -684,6 +684,7 @@ __global__ void math_probe(int op, const double* x, const double* y, int n, doub
     case 7: r = log(a); break;
     case 8: r = pow(a, b); break;
     case 9: r = ghc_atan2(a, b); break;
+    case 11: r = pow5(a); break;
     default: r = tan(a); break;
   }
   out[i] = r;
@@ -1499,7 +1500,7 @@ int rt_debug_closest_hits(rt_ctx* c, const double* rays, int n, double tmin, dou
 }
 
 int rt_debug_math(rt_ctx* c, int op, const double* x, const double* y, int n, double* out) {
-  if (!c || !x || !y || !out || n < 0 || op < 0 || op > 10) return invalid("rt_debug_math: bad argument");
+  if (!c || !x || !y || !out || n < 0 || op < 0 || op > 11) return invalid("rt_debug_math: bad argument");
   if (n == 0) return RT_OK;
   HIPCHK(hipSetDevice(c->device));
   double *dx = nullptr, *dy = nullptr, *dout = nullptr;

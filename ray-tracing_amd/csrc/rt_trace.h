@@ -999,10 +999,31 @@ __device__ __forceinline__ V3 refract(V3 v, V3 n, double eta) {
   const V3 perp = scale(-sqrt(1.0 - sqlen(par)), n);
   return par + perp;
 }
+// x ** 5 for schlick (Lib.hs:903, libm pow on the reference's side). x^2, x^4 and x^5 are carried
+// as unevaluated sums hi + lo (each product's rounding error recovered exactly by an FMA), so the
+// one final rounding is correct except within ~2^-100 relative of a rounding midpoint: the result
+// is the correctly rounded x^5 (glibc's pow is within 0.52 ulp of it; OCML's pow(x, 5) matched
+// glibc in 76 % of cases). No polynomial constants either: the compiler hoisted OCML pow's into
+// registers for the whole kernel and spilled them. Zeros, NaN, infinities and magnitudes outside
+// [2^-200, 2^200] (x = 1 - cos theta lies in [0, 2]) take the plain product.
+__device__ __forceinline__ double pow5(double x) {
+  const double ax = fabs(x);
+  if (!(ax >= 0x1p-200 && ax <= 0x1p200)) return x * x * x * x * x;
+  const double h2 = x * x, l2 = fma(x, x, -h2);
+  double h4 = h2 * h2, l4 = fma(h2, h2, -h4);
+  l4 = fma(2.0 * h2, l2, l4);  // (h2 + l2)^2 = h2^2 + 2 h2 l2 (+ l2^2, below 2^-104 relative)
+  const double s4 = h4 + l4;
+  l4 = l4 - (s4 - h4);
+  h4 = s4;
+  const double h5 = h4 * x;
+  double l5 = fma(h4, x, -h5);
+  l5 = fma(l4, x, l5);
+  return h5 + l5;
+}
 __device__ __forceinline__ double schlick(double cosine, double ref_idx) {
   const double r0 = (1.0 - ref_idx) / (1.0 + ref_idx);
   const double r1 = r0 * r0;
-  return r1 + (1.0 - r1) * pow(1 - cosine, 5.0);
+  return r1 + (1.0 - r1) * pow5(1 - cosine);
 }
 
 struct Scatter {

@@ -36,7 +36,7 @@ RT_DEBUG_RESUMABLE = 4  # rt_debug_closest_hits: the render loop's resumable bin
 RT_DEBUG_WIDE = 8       # rt_debug_closest_hits: the resumable walk over the 4-wide fp32-box tree
 RT_BVH_ORDERED = 0x40000000
 MATH_OPS = {"div": 0, "div_exact": 1, "sqrt": 2, "sin": 3, "cos": 4, "atan": 5, "asin": 6, "log": 7, "pow": 8,
-            "ghc_atan2": 9, "tan": 10}
+            "ghc_atan2": 9, "tan": 10, "pow5": 11}
 
 XYPlane, XZPlane, YZPlane = 0, 1, 2
 XAxis, YAxis, ZAxis = 0, 1, 2
