@@ -282,8 +282,10 @@ def main():
                                "traffic_note": tnote,
                                "kernel_ms": round(kernel_avg, 3),
                                "bytes_per_sample": round(bytes_per_sample, 2),
-                               "note": "algorithmic scene-record bytes per sample, device-counted by the counting "
-                                       "build of the same launch; the binding roof is FP64 VALU (see fp64)"}
+                               "note": "achieved = algorithmic scene-record bytes (4-wide nodes, leaves, materials) "
+                                       "per sample, device-counted by the counting build of the same launch, over "
+                                       "the kernel time; they are served from LDS and L2, not HBM (traffic = the "
+                                       "PMC-measured HBM bytes). The binding roof is VALU issue (see fp64/fp32)"}
             out["fp64"] = {"achieved_tflops": round(fl, 3), "peak_tflops": FP64_PEAK_TFLOPS,
                            "frac": round(fl / FP64_PEAK_TFLOPS, 5), "flops_per_sample": round(flops_per_sample, 1)}
             f32 = sum(FLOPS32[k] * per.get(k, 0) for k in FLOPS32)

@@ -172,17 +172,23 @@ typedef struct rt_camera {
  *                counter = {draw_pair, sample, pixel_id, 0}; each 128-bit block yields two
  *                64-bit words, converted exactly as random-1.2.0 `random :: Double`.
  *                A pixel's samples are summed in fixed chunks: chunk k holds samples
- *                [k*CH, min(spp, (k+1)*CH)) with CH = rt_sample_chunk(spp) = min(spp,
- *                RT_CHUNK_SAMPLES); each chunk is summed in sample order from 0, the chunk sums
- *                in chunk order from 0. (The chunks are the device's work-items; a fixed
- *                definition keeps the image independent of scheduling and shard count.)
- *                Embarrassingly parallel.
+ *                [k*CH, min(spp, (k+1)*CH)) with CH = rt_sample_chunk(width*height, spp);
+ *                each chunk is summed in sample order from 0, the chunk sums in chunk order
+ *                from 0. (The chunks are the device's work-items; a definition fixed by
+ *                (width, height, spp) keeps the image independent of scheduling and shard
+ *                count.) Embarrassingly parallel.
  */
 #define RT_RNG_EXACT 0
 #define RT_RNG_PHILOX 1
-#define RT_CHUNK_SAMPLES 32 /* samples per chunk (C2 on MI355X: 186.4 ms at 32, 187.6 at 64, 205 at 16) */
-static inline int rt_sample_chunk(int spp) {
-  return spp < RT_CHUNK_SAMPLES ? (spp > 0 ? spp : 1) : RT_CHUNK_SAMPLES;
+#define RT_CHUNK_SAMPLES 32  /* samples per chunk (C2 on MI355X: 186.4 ms at 32, 187.6 at 64, 205 at 16) */
+#define RT_CHUNK_ITEMS (1 << 20) /* ...fewer when the frame would have fewer work-items than this */
+/* CH = min(spp, 32, max(1, ceil(pixels * spp / 2^20))): 32-sample chunks, except that small frames
+   (e.g. config 1: 200x100x10) use shorter ones so that they still fill the device. */
+static inline int rt_sample_chunk(int64_t pixels, int spp) {
+  const int64_t fill = (pixels * (int64_t)spp + RT_CHUNK_ITEMS - 1) / RT_CHUNK_ITEMS;
+  int ch = spp < RT_CHUNK_SAMPLES ? spp : RT_CHUNK_SAMPLES;
+  if (fill < ch) ch = (int)fill;
+  return ch > 0 ? ch : 1;
 }
 
 /* Flags. */

@@ -669,7 +669,7 @@ static V3 render_pixel_exact(const Ctx* c, int x, int y, Rng* g, double* uvbuf) 
    within fixed chunks, chunk sums in chunk order (include/rt.h, rt_sample_chunk). */
 static V3 render_pixel_philox(const Ctx* c, int x, int y, uint32_t pid, uint64_t seed, int64_t* draws) {
     V3 acc = v3(0, 0, 0);
-    const int ch = rt_sample_chunk(c->spp);
+    const int ch = rt_sample_chunk((int64_t)c->width * c->height, c->spp);
     for (int k0 = 0; k0 < c->spp; k0 += ch) {
         V3 part = v3(0, 0, 0);
         const int k1 = k0 + ch < c->spp ? k0 + ch : c->spp;

@@ -1034,7 +1034,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   A.shard_rank = rank;
   A.shard_count = shards;
   A.slab = slab;
-  A.chunk = rt_sample_chunk(p->spp);
+  A.chunk = rt_sample_chunk((int64_t)p->width * p->height, p->spp);
   A.chunks = (p->spp + A.chunk - 1) / A.chunk;
   A.work_total = slab * A.chunks;
   if (A.work_total >= (1ll << 32)) return invalid("image too large: more than 2^32 work-items per shard");

@@ -55,13 +55,14 @@ def test_book_one_tier_b(gpu_ctx):
     _cmp(gpu_ctx, sc, cam, p)
 
 
-@pytest.mark.parametrize("spp", [33, 70])
-def test_tier_b_sample_chunks(gpu_ctx, spp):
-    """spp > RT_CHUNK_SAMPLES: a pixel's samples are summed per chunk (rt_sample_chunk), chunk sums
-    in chunk order — the device's work-items, combined by `combine_chunks` — exactly as the oracle."""
+@pytest.mark.parametrize("w,h,spp", [(32, 24, 33), (64, 64, 600), (128, 96, 700)])
+def test_tier_b_sample_chunks(gpu_ctx, w, h, spp):
+    """A pixel's samples are summed per chunk (rt_sample_chunk: 1, 3 and 9 samples here), chunk
+    sums in chunk order — the device's work-items, combined by `combine_chunks` — exactly as the
+    oracle."""
     sc, _ = _scene("random_book_one")
-    cam = rtamd.camera("random_scene", 32, 24)
-    p = rtamd.make_params(32, 24, spp, 50, rtamd.RT_RNG_PHILOX, seed=3)
+    cam = rtamd.camera("random_scene", w, h)
+    p = rtamd.make_params(w, h, spp, 50, rtamd.RT_RNG_PHILOX, seed=3)
     rgb_g, lin_g, _, _ = _cmp(gpu_ctx, sc, cam, p)
     rgb_o, lin_o, _, _ = pyoracle.render(sc, cam, p)
     close = np.isclose(lin_g, lin_o, rtol=1e-12, atol=0, equal_nan=True).mean()
