@@ -1034,18 +1034,52 @@ struct Scatter {
 };
 
 // scatter for every material except DiffuseLight (which the caller turns into `emitted`).
+// The branches are fused where the materials compute the same thing, so that a wave holding
+// several materials runs the expensive parts once: Lambertian's cosine sample
+// (random_cosine_direction, Lib.hs:1206-1217) and Metal's fuzz vector (random_unit_vector,
+// Lib.hs:1187-1197) both draw two numbers and take the cosine and sine of 2*pi*(first draw) —
+// `2.0 * pi * r1` and `aa * 2.0 * pi` round identically, doubling being exact — and one square
+// root; Metal and Dielectric both start from `unit(r.d)`. Each lane's draws keep the reference's
+// order (Lambertian: coin, then its branch's draws).
 template <unsigned F, class R>
 __device__ __forceinline__ void scatter(const Scene& S, const DMat& m, const Ray& r, const Hit& h, R& g, Scatter& s) {
   s.ray.o = h.p;
   s.ray.tm = r.tm;
   g.reserve(3);  // Lambertian draws 1 or 3 (more when sampling a lights BVH), Metal 2, Dielectric 1
-  if (m.type == RT_MAT_LAMBERTIAN) {  // Lib.hs:823-836, mixture of light and cosine pdfs
+  const bool lamb = m.type == RT_MAT_LAMBERTIAN, metal = m.type == RT_MAT_METAL;
+  const bool diel = m.type == RT_MAT_DIELECTRIC;
+  if (!(lamb || metal || diel)) {  // RT_MAT_ISOTROPIC, Lib.hs:861-865
+    s.ray.d = random_in_unit_sphere(g);
     s.att = texture_value<F>(S, m.tex, h.u, h.v, h.p);
-    const ONB uvw = onb_from_w(h.n);
-    const double rd = g.draw();
-    V3 pdf_d;
-    if (rd < 0.5) pdf_d = (F & F_LIGHTS) ? htbl_random(S, S.lights, h.p, g) : v3(1, 0, 0);
-    else pdf_d = onb_local(uvw, random_cosine_direction(g));
+    s.pdf = 1.0;
+    s.specular = 0;
+    return;
+  }
+  ONB uvw{};
+  double coin = 1.0;
+  if (lamb) {  // Lib.hs:823-836, mixture of light and cosine pdfs: the coin comes first
+    uvw = onb_from_w(h.n);
+    coin = g.draw();
+  }
+  const bool light = lamb && coin < 0.5;
+  V3 v = v3(1, 0, 0);  // the cosine-weighted sample (Lambertian) or the unit vector (Metal)
+  if (metal || (lamb && !light)) {
+    const double a = g.draw(), b = g.draw();
+    const double ang = 2.0 * kPi * a;
+    const double cs = cos(ang), sn = sin(ang);
+    const double z = (b * 2.0) - 1.0;                      // Metal: z = 2 zz - 1
+    const double q = sqrt(metal ? 1.0 - z * z : 1.0 - b);  // Metal: r; Lambertian: z
+    const double sr2 = sqrt(b);
+    if (metal) v = v3(q * cs, q * sn, z);
+    else v = onb_local(uvw, v3(cs * sr2, sn * sr2, q));
+  }
+  V3 ud = v3(0, 0, 0);
+  if (metal || diel) ud = unit(r.d);
+  if (lamb) {
+    s.att = texture_value<F>(S, m.tex, h.u, h.v, h.p);
+    V3 pdf_d = v;
+    if constexpr ((F & F_LIGHTS) != 0)
+      if (light) pdf_d = htbl_random(S, S.lights, h.p, g);
     const V3 dir = unit(pdf_d);
     s.ray.d = dir;
     double v1 = 0.0;
@@ -1055,16 +1089,14 @@ __device__ __forceinline__ void scatter(const Scene& S, const DMat& m, const Ray
     const double v2 = cosine <= 0 ? 0 : cosine / kPi;
     s.pdf = 0.5 * (v1 + v2);
     s.specular = 0;
-  } else if (m.type == RT_MAT_METAL) {  // Lib.hs:837-841
-    const V3 r_unit = random_unit_vector(g);
-    const V3 reflected = reflect(unit(r.d), h.n);
-    s.ray.d = reflected + scale(m.param, r_unit);
+  } else if (metal) {  // Lib.hs:837-841
+    const V3 reflected = reflect(ud, h.n);
+    s.ray.d = reflected + scale(m.param, v);
     s.att = texture_value<F>(S, m.tex, h.u, h.v, h.p);
     s.pdf = 0.0;
     s.specular = 1;
-  } else if (m.type == RT_MAT_DIELECTRIC) {  // Lib.hs:842-859
+  } else {  // Dielectric, Lib.hs:842-859
     const double eta = h.ff ? 1.0 / m.param : m.param;
-    const V3 ud = unit(r.d);
     const double cos_theta = gmin(dot(vneg(ud), h.n), 1.0);
     const double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
     const double rd = g.draw();
@@ -1073,11 +1105,6 @@ __device__ __forceinline__ void scatter(const Scene& S, const DMat& m, const Ray
     s.att = v3(1.0, 1.0, 1.0);
     s.pdf = 1.0;
     s.specular = 1;
-  } else {  // RT_MAT_ISOTROPIC, Lib.hs:861-865
-    s.ray.d = random_in_unit_sphere(g);
-    s.att = texture_value<F>(S, m.tex, h.u, h.v, h.p);
-    s.pdf = 1.0;
-    s.specular = 0;
   }
 }
 
