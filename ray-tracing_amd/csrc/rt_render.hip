@@ -413,6 +413,10 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
       trav_restart_ref(t, S.world_ref, INFINITY);
       walking = true;
     }
+    // the next walk's ray: a scattered ray (next segment) or a camera ray (next sample), parked in
+    // t.ray (free once the walk's hit is recorded); both kinds of lane start their walk together
+    // below, so the walk set-up runs once per wave
+    bool start = false;
     if (ready) {
       ready = false;
       Hit h;
@@ -424,15 +428,16 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
       } else if (depth <= 0) {  // rayColor's d <= 0 -> black (thr * 0 keeps a NaN throughput NaN)
         end_sample(vmul(thr, v3(0.0, 0.0, 0.0)));
       } else {  // next segment of the same path
-        trav_begin<F>(t, ray, S.world, kEps, INFINITY);
-        if (S.ref_walk) trav_restart_ref(t, S.world_ref, INFINITY);
-        walking = true;
+        t.ray.o = ray.o;
+        t.ray.d = ray.d;
+        t.ray.tm = ray.tm;
+        start = true;
         if constexpr ((F & F_COUNT) != 0) ++segs;
       }
     }
     unsigned long long s0b = 0;
     if constexpr ((F & F_COUNT) != 0) s0b = stamp();
-    while (!walking) {
+    while (!walking && !start) {
       // acquire pixels for idle lanes: one atomic per round for all of them
       for (;;) {
         const bool need = (w < 0) && !done;
@@ -462,17 +467,23 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
       const int y = A.H - 1 - row;
       const double u = ((double)px + ru) / (double)A.W;
       const double v = ((double)y + rv) / (double)A.H;
-      const Ray ray = get_ray(A.cam, u, v, g);
+      const Ray cray = get_ray(A.cam, u, v, g);
+      t.ray.o = cray.o;
+      t.ray.d = cray.d;
+      t.ray.tm = cray.tm;
       thr = v3(1.0, 1.0, 1.0);
       depth = A.max_depth;
       if (depth <= 0) {
         end_sample(vmul(thr, v3(0.0, 0.0, 0.0)));
         continue;
       }
-      trav_begin<F>(t, ray, S.world, kEps, INFINITY);
+      start = true;
+      if constexpr ((F & F_COUNT) != 0) ++segs;
+    }
+    if (start) {
+      trav_begin<F>(t, plain(t.ray), S.world, kEps, INFINITY);
       if (S.ref_walk) trav_restart_ref(t, S.world_ref, INFINITY);
       walking = true;
-      if constexpr ((F & F_COUNT) != 0) ++segs;
     }
     if (!walking) break;  // this lane is finished; the rest of the wave carries on without it
     unsigned long long s1 = 0;
