@@ -1,16 +1,18 @@
 // rt_render.hip — render kernels for gfx950 and the device half of the C ABI (include/rt.h).
 //
-// Kernel design (DESIGN.md §Kernels):
-//  * one work-item = one pixel; a lane keeps its pixel until all `spp` samples are summed, in
-//    sample order, so each pixel's sum is formed exactly as renderPos does (Lib.hs:1343-1350);
-//  * persistent waves with path regeneration: every loop iteration traces ONE segment for every
-//    live lane; a lane whose path ended starts its next sample (or fetches a new pixel through
-//    one wave-aggregated atomicAdd on a work counter) at the top of the next iteration, so
-//    lanes never idle waiting for the longest path of a sample;
+// Kernel design (DESIGN.md §3):
+//  * tier B work-items are (pixel, chunk of up to 32 samples): a lane sums its chunk in sample
+//    order and stores the sum; `combine_chunks` adds a pixel's chunk sums in chunk order (rt.h);
+//  * persistent waves with ray replacement (`philox_loop2`): the closest-hit walk is resumable;
+//    each iteration shades the lanes whose walk ended and starts their next segment, sample or
+//    work-item (one wave-aggregated atomicAdd on a work counter), then steps the walking lanes
+//    until few still walk — a wave never waits for its slowest walk;
+//  * the 4-wide fp32-box walk postpones leaves so wide-node steps and fp64 leaf tests do not
+//    share a divergent step; worlds with media or instance frames walk the caller's tree in the
+//    reference's own order (media draws);
 //  * forward throughput (thr *= att * (spdf / pdf)) instead of the reference's continuation;
 //    colour never feeds control flow or the RNG, so this changes rounding only;
-//  * the BVH traversal stack lives in LDS, [entry][lane] so consecutive lanes hit consecutive
-//    banks;
+//  * traversal stacks live in LDS, [entry][lane] so consecutive lanes hit consecutive banks;
 //  * tier B (Philox per (pixel, sample)) shards by tiles with no data-path collective; tier A
 //    (the reference's per-column SplitMix stream) runs one lane per column.
 #include <hip/hip_runtime.h>
@@ -930,15 +932,13 @@ unsigned variant_for(unsigned f) {
   if ((f & ~kVarCornell) == 0) return kVarCornell;
   return F_ALL;
 }
-// Occupancy target (waves per SIMD) of the render kernel; RTAMD_WAVES overrides (2, 3 or 4) for
-// A/B measurements.
-// Defaults: the largest occupancy that compiles without scratch spills (make resources).
+// Occupancy target (waves per SIMD) of the render kernel; RTAMD_WAVES overrides (1..4) for A/B
+// measurements. The defaults (launch_philox) are measured.
 int waves_target(int dflt) {
   const char* e = std::getenv("RTAMD_WAVES");
   const int w = e ? std::atoi(e) : dflt;
   return (w >= 1 && w <= 4) ? w : dflt;
 }
-// Kernel pointer for (variant, replacement loop?, LDS-staged?, waves per SIMD, counting build?).
 // Kernel pointer for (variant, loop, LDS-staged?, waves per SIMD, counting build?); loop 0 = one
 // sample per lane walk, 1 = ray replacement over the binary tree, 2 = replacement over the
 // 4-wide tree.
