@@ -40,6 +40,7 @@ MATH_OPS = {"div": 0, "div_exact": 1, "sqrt": 2, "sin": 3, "cos": 4, "atan": 5, 
 
 XYPlane, XZPlane, YZPlane = 0, 1, 2
 XAxis, YAxis, ZAxis = 0, 1, 2
+RT_OK, RT_E_INVALID, RT_E_HIP, RT_E_NOMEM, RT_E_UNSUPPORTED, RT_E_STATE = 0, -1, -2, -3, -4, -5
 
 SCENES = {
     "cornell": 0, "cornell_smoke": 1, "simple_light": 2, "earth": 3, "two_perlin_spheres": 4,

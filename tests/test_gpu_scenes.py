@@ -1,0 +1,100 @@
+"""GPU: scenes built through the reference's constructor API (rtamd.Builder, the src/Lib.hs
+surface) that exercise the device path's structural limits — instance frames nested within and
+beyond RT_MAX_FRAMES (replacement loop vs per-sample loop), media inside frames — and the
+upload's validation of malformed descriptors (error codes, no fallback)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import pyoracle
+import rtamd
+from conftest import parity
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames_scene(depth, medium=False):
+    """Ground + a BVH of small spheres wrapped in `depth` alternating Translate/Rotate frames
+    (Lib.hs:561-576) + optionally a ConstantMedium inside the frames, all under makeBVH."""
+    b = rtamd.Builder(rtamd.randGen(77))
+    white = b.lambertian(b.constantColor(0.73, 0.73, 0.73))
+    red = b.lambertian(b.constantColor(0.65, 0.05, 0.05))
+    glass = b.dielectric(1.5)
+    metal = b.metal(b.constantColor(0.8, 0.8, 0.9), 0.1)
+    rng = np.random.default_rng(3)
+    items = []
+    for i in range(24):
+        c = (float(rng.uniform(-2, 2)), float(rng.uniform(0.2, 2)), float(rng.uniform(-2, 2)))
+        items.append(b.sphere(c, float(rng.uniform(0.1, 0.4)), [white, red, glass, metal][i % 4]))
+    if medium:
+        boundary = b.sphere((0.0, 1.0, 0.0), 0.8, glass)
+        items.append(b.constantMedium(0.6, b.constantColor(0.2, 0.4, 0.9), boundary))
+    inner = b.makeBVH((0.0, 1.0), items)
+    for k in range(depth):
+        inner = b.translate((0.3, 0.0, -0.2), inner) if k % 2 == 0 else b.rotate(rtamd.YAxis, 17.0, inner)
+    ground = b.sphere((0.0, -1000.0, 0.0), 1000.0, white)
+    world = b.makeBVH((0.0, 1.0), [ground, inner])
+    return b.finish(world, -1, (0.7, 0.8, 1.0))
+
+
+@pytest.mark.parametrize("depth,medium", [(2, False), (2, True), (6, False)])
+def test_nested_frames(gpu_ctx, depth, medium, monkeypatch):
+    """Frames nested 2 deep (replacement loop, Side slots) and 6 deep (> RT_MAX_FRAMES: per-sample
+    loop), with a medium inside the frames: the oracle's image within the tolerance, and the two
+    loops byte-identical where both apply."""
+    sc = _frames_scene(depth, medium)
+    cam = rtamd.camera("random_scene", 64, 40)
+    p = rtamd.make_params(64, 40, 6, 20, rtamd.RT_RNG_PHILOX, seed=9)
+    gpu_ctx.upload(sc)
+    rgb, lin, _ = gpu_ctx.render(cam, p, linear=True)
+    rgb_o, lin_o, _, _ = pyoracle.render(sc, cam, p)
+    ok, eq, dmax = parity(lin, lin_o, rgb, rgb_o)
+    assert ok >= 0.995 and eq >= 0.995, (ok, eq, dmax)
+    monkeypatch.setenv("RTAMD_REPLACE", "0")
+    rgb_s, lin_s, _ = gpu_ctx.render(cam, p, linear=True)
+    assert np.array_equal(rgb, rgb_s) and np.array_equal(lin, lin_s, equal_nan=True)
+
+
+def _desc_with_nodes(sc, nodes, **over):
+    """A copy of scene `sc`'s descriptor pointing at `nodes` (kept alive by the caller)."""
+    d = rtamd.rt_scene_desc()
+    C.pointer(d)[0] = sc.desc
+    d.nodes = nodes.ctypes.data_as(C.POINTER(rtamd.rt_node))
+    d.n_nodes = len(nodes)
+    for k, v in over.items():
+        setattr(d, k, v)
+    return d
+
+
+def _upload_raw(ctx, d):
+    return rtamd.lib().rt_upload_scene(ctx._h, C.byref(d))
+
+
+def test_upload_rejects_malformed_scenes(gpu_ctx):
+    """rt_upload_scene validates the DAG and its references: RT_E_INVALID for a child that does not
+    precede its parent, a material or root out of range; RT_E_UNSUPPORTED for a medium in the
+    lights tree. A rejected upload leaves the previously uploaded scene in place, untouched."""
+    sc, _ = rtamd.make_scene("cornell", rtamd.randGen(1024))
+    cam = rtamd.camera("cornell", 16, 16)
+    p = rtamd.make_params(16, 16, 2, 10, rtamd.RT_RNG_PHILOX, seed=4)
+    gpu_ctx.upload(sc)
+    before, _, _ = gpu_ctx.render(cam, p)
+    base = np.array(sc.nodes, copy=True)
+    bvh = np.where(base["type"] == rtamd.RT_NODE_BVH)[0][0]
+    bad = base.copy()
+    bad["a"][bvh] = len(bad) - 1 if len(bad) - 1 > bvh else bvh  # child at or after its parent
+    assert _upload_raw(gpu_ctx, _desc_with_nodes(sc, bad)) == rtamd.RT_E_INVALID
+    assert b"precede" in rtamd.lib().rt_last_error()
+    bad = base.copy()
+    sph = np.where(np.isin(base["type"], [rtamd.RT_NODE_RECT_XZ, rtamd.RT_NODE_SPHERE]))[0][0]
+    bad["a"][sph] = 10_000  # material out of range
+    assert _upload_raw(gpu_ctx, _desc_with_nodes(sc, bad)) == rtamd.RT_E_INVALID
+    assert _upload_raw(gpu_ctx, _desc_with_nodes(sc, base, world_root=len(base) + 5)) == rtamd.RT_E_INVALID
+    smoke, _ = rtamd.make_scene("cornell_smoke", rtamd.randGen(1024))
+    snodes = np.array(smoke.nodes, copy=True)
+    medium = int(np.where(snodes["type"] == rtamd.RT_NODE_CONSTANT_MEDIUM)[0][0])
+    rc = _upload_raw(gpu_ctx, _desc_with_nodes(smoke, snodes, lights_root=medium))
+    assert rc == rtamd.RT_E_UNSUPPORTED, rc
+    after, _, _ = gpu_ctx.render(cam, p)
+    assert np.array_equal(before, after)
