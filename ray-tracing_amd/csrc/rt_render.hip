@@ -1074,7 +1074,9 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   const char* stop_env = std::getenv("RTAMD_TRAV_STOP");
   // refill when at most trav_stop/64 of a wave's live lanes still walk (measured: C2 flat at 2-8,
   // -4 % at 16; the 100k-sphere C5 tree, walks ~3x longer, best at 16)
-  A.trav_stop = stop_env ? std::max(0, std::min(63, std::atoi(stop_env))) : (c->n_nodes > 20000 ? 16 : 8);
+  // (the full variant's walks over the caller's tree: 16, C4 1496 vs 1567 ms at 200 spp)
+  A.trav_stop = stop_env ? std::max(0, std::min(63, std::atoi(stop_env)))
+                         : (c->n_nodes > 20000 || variant_for(c->features) == F_ALL ? 16 : 8);
   const char* leaf_env = std::getenv("RTAMD_LEAF_STOP");
   // leaf steps once <= that many lanes still seek their first leaf (measured: C2 212.6 ms at 6-8/64
   // vs 219.7 at 0 and 232 without postponement; C5 (16 spp) 219.9 ms at 16/64 vs 326 at 0)
@@ -1093,24 +1095,33 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   // (the full variant has no 4-wide instantiation: its media-free worlds walk the binary tree)
   const bool wide = replace && c->d_wnodes && !(p->flags & RT_FLAG_REFERENCE_CULL) && want_wide && var != F_ALL;
   const int loop = wide ? 2 : (replace ? 1 : 0);
-  // waves per SIMD (measured): spheres 3 (C2 -11 % at 2, -9 % at 4; C5 -15 % at 2); Cornell-like
-  // on the replacement loop 3 (C3 380.5 ms vs 453.7 at 2, 428.6 at 4), 1 on the per-sample loop;
-  // full variant on the replacement loop 3 (C4 at 100 spp: 90.9 vs 87.5 Msamples/s at 2), on the
+  // waves per SIMD (measured): spheres 4 when the LDS-staged kernel fits at 4 (C2 158.4 ms vs
+  // 166.6 at 3, 203.2 at 2), else 3 (C5 186.7 ms vs 228.5 at 4, -15 % at 2); Cornell-like on the
+  // replacement loop 3 (C3 359.6 ms vs 374.3 at 4, 453.3 at 2), 1 on the per-sample loop; full
+  // variant on the replacement loop 3 (C4 at 100 spp: 90.9 vs 87.5 Msamples/s at 2), on the
   // per-sample loop 2 despite 784 B/lane of scratch (C4 35.2 vs 23.4 at 1 wave, 9.1 at 3)
-  const int waves = (var == kVarSpheres || loop) ? waves_target(3) : waves_target(var == F_ALL ? 2 : 1);
+  int waves = (var == kVarSpheres || loop) ? waves_target(3) : waves_target(var == F_ALL ? 2 : 1);
   const int side_ints = (var & F_FRAMES) && loop == 1 ? kSideInts : 0;  // Side slots after the stacks
   // LDS-staged kernel when the traversal's node array plus the stacks fit one CU's 160 KiB
   // (RTAMD_LDS=0 disables it for A/B runs).
   if (!count && !env_off("RTAMD_LDS") && (var != F_ALL || loop)) {
-    const int block = waves * 256;
     const int entries = wide ? c->wide_stack_need + 3 : c->stack_need + 2;  // (wide_node writes 3 slots)
     const int items = wide ? c->n_wnodes : c->n_nodes;
     const size_t rec = wide ? sizeof(rt_wnode) : sizeof(rt_node);
-    size_t bytes = (size_t)items * rec + (size_t)(entries + side_ints) * block * sizeof(int);
-    // the wide walk's leaf table joins the nodes in LDS when it fits as well (RTAMD_LEAF_LDS=0: never)
-    int n_leaves = wide && !env_off("RTAMD_LEAF_LDS") ? c->n_leaves : 0;
-    if (bytes + (size_t)n_leaves * sizeof(rt_node) > 160 * 1024) n_leaves = 0;
-    bytes += (size_t)n_leaves * sizeof(rt_node);
+    const bool leaf_lds = wide && !env_off("RTAMD_LEAF_LDS");  // RTAMD_LEAF_LDS=0: leaves never in LDS
+    // LDS bytes at `w` waves per SIMD: the nodes, the lane stacks, and the wide walk's leaf table
+    // when it fits as well
+    auto lds_bytes = [&](int w, int& n_leaves) {
+      size_t b = (size_t)items * rec + (size_t)(entries + side_ints) * (w * 256) * sizeof(int);
+      n_leaves = leaf_lds && b + (size_t)c->n_leaves * sizeof(rt_node) <= 160 * 1024 ? c->n_leaves : 0;
+      return b + (size_t)n_leaves * sizeof(rt_node);
+    };
+    int n_leaves = 0;
+    if (var == kVarSpheres && !std::getenv("RTAMD_WAVES") && lds_bytes(4, n_leaves) <= 160 * 1024 &&
+        (!leaf_lds || n_leaves > 0))
+      waves = 4;
+    const int block = waves * 256;
+    const size_t bytes = lds_bytes(waves, n_leaves);
     if (bytes <= 160 * 1024) {
       const void* fn = philox_kernel(var, loop, true, waves, false);
       HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
