@@ -1117,8 +1117,9 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
       return b + (size_t)n_leaves * sizeof(rt_node);
     };
     int n_leaves = 0;
+    // (and only when there is work for the 4th wave: C1's 20 000 items fill less than 3 waves)
     if (var == kVarSpheres && !std::getenv("RTAMD_WAVES") && lds_bytes(4, n_leaves) <= 160 * 1024 &&
-        (!leaf_lds || n_leaves > 0))
+        (!leaf_lds || n_leaves > 0) && A.work_total >= (long long)c->cu_count * 1024)
       waves = 4;
     const int block = waves * 256;
     const size_t bytes = lds_bytes(waves, n_leaves);
