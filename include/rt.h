@@ -319,6 +319,10 @@ int rt_rebuild_bvh(const rt_scene_desc* desc, rt_node* out_nodes, int capacity, 
  * = the walk's stack bound (entries). RT_E_UNSUPPORTED when the root is not a BVH node. */
 int rt_wide_bvh(const rt_node* nodes, int n_nodes, int root, void* out, int capacity, int* out_n,
                 int* out_stack_need);
+/* Stack entries the binary walk over the tree at `root` needs (the bound rt_upload_scene sizes
+ * the LDS stacks with): left-first for the caller's nodes, either child first for rebuilt
+ * (RT_BVH_ORDERED) nodes, one entry per open instance frame. */
+int rt_tree_stack_need(const rt_node* nodes, int n_nodes, int root, int* out_need);
 
 /*
  * Blocking full-image render (replaces runRender, src/Lib.hs:1491).

@@ -24,6 +24,7 @@ namespace rt {
 namespace {
 
 constexpr double kEps = 0.0001;
+constexpr int kMaxStackNeed = 30;  // RT_STACK - 2 (rt_device.h): the upload validator's bound
 inline double gmax(double x, double y) { return x <= y ? y : x; }
 inline double gmin(double x, double y) { return x <= y ? x : y; }
 
@@ -222,6 +223,42 @@ bool flat_box(const std::vector<rt_node>& nodes, int id, Box* out) {
   }
 }
 
+// Per-node traversal-stack needs (entries) over a flat node array whose children precede their
+// parents: the recurrence rt_upload_scene's validator applies (bvh_stack_need for BVH nodes, one
+// entry per open instance frame, 0 for primitives and Translate/Rotate chains over one). False
+// when a child does not precede its parent.
+bool stack_needs(const std::vector<rt_node>& nodes, std::vector<int>& need) {
+  const int n = (int)nodes.size();
+  need.assign(n, 0);
+  std::vector<char> chain(n, 0);
+  for (int i = 0; i < n; ++i) {
+    const rt_node& x = nodes[i];
+    switch (x.type) {
+      case RT_NODE_BVH:
+        if (x.a < 0 || x.a >= i || x.b < 0 || x.b >= i) return false;
+        need[i] = bvh_stack_need(x, need[x.a], need[x.b]);
+        break;
+      case RT_NODE_TRANSLATE:
+      case RT_NODE_ROTATE:
+        if (x.a < 0 || x.a >= i) return false;
+        if (chain[x.a]) chain[i] = 1;
+        else need[i] = 1 + need[x.a];
+        break;
+      case RT_NODE_SPHERE:
+      case RT_NODE_MOVING_SPHERE:
+      case RT_NODE_RECT_XY:
+      case RT_NODE_RECT_XZ:
+      case RT_NODE_RECT_YZ:
+      case RT_NODE_CUBOID:
+        chain[i] = 1;
+        break;
+      default:
+        break;
+    }
+  }
+  return true;
+}
+
 // Rebuild the world tree rooted at `root` over its leaves; appends nodes, returns the new root
 // (or `root` unchanged when the tree is not eligible). Eligible: no ConstantMedium anywhere
 // under the root, every leaf boundable, finite boxes.
@@ -273,7 +310,16 @@ int rebuild_world_bvh(std::vector<rt_node>& nodes, int root) {
   std::vector<int> items(n);
   for (int i = 0; i < n; ++i) items[i] = i;
   Box rb;
-  return b.build(items, 0, n, rb);
+  const size_t n_before = nodes.size();
+  const int new_root = b.build(items, 0, n, rb);
+  // A degenerate split sequence (e.g. exponentially spaced centroids) can give a spine deeper than
+  // the LDS traversal stack; keep the caller's tree then.
+  std::vector<int> need;
+  if (!stack_needs(nodes, need) || need[new_root] > kMaxStackNeed) {
+    nodes.resize(n_before);
+    return root;
+  }
+  return new_root;
 }
 
 namespace {
@@ -393,6 +439,20 @@ extern "C" int rt_rebuild_bvh(const rt_scene_desc* in, rt_node* out_nodes, int c
     }
     std::copy(nodes.begin(), nodes.end(), out_nodes);
   }
+  return RT_OK;
+}
+
+extern "C" int rt_tree_stack_need(const rt_node* nodes, int n_nodes, int root, int* out_need) {
+  if (!nodes || n_nodes <= 0 || root < 0 || root >= n_nodes || !out_need) {
+    rt::set_error("rt_tree_stack_need: bad argument");
+    return RT_E_INVALID;
+  }
+  std::vector<int> need;
+  if (!rt::stack_needs(std::vector<rt_node>(nodes, nodes + n_nodes), need)) {
+    rt::set_error("rt_tree_stack_need: a child must precede its parent");
+    return RT_E_INVALID;
+  }
+  *out_need = need[root];
   return RT_OK;
 }
 

@@ -46,6 +46,15 @@ struct Box {
   double mn[3], mx[3];
 };
 
+// Traversal-stack entries a BVH node needs (rt_trace.h traverse / walk_step), given its
+// children's needs. Caller's (makeBVH) nodes are walked left first, with b waiting on the stack
+// while a is walked (hit BVHNode, src/Lib.hs:971-988). A rebuilt node (RT_BVH_ORDERED) enters the
+// child on the ray's side of the split first, so either child can be walked above the other.
+inline int bvh_stack_need(const rt_node& x, int need_a, int need_b) {
+  if (x.c & RT_BVH_ORDERED) return 1 + (need_a > need_b ? need_a : need_b);
+  return (1 + need_a > need_b) ? 1 + need_a : need_b;
+}
+
 }  // namespace rt
 
 struct rt_builder {

@@ -712,6 +712,9 @@ struct rt_ctx {
   int blocks_per_cu = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // Recorded after every tier-B launch: the next launch (on any stream) waits on it before it
+  // resets the shared work counter and reuses the chunk-sum buffer.
+  hipEvent_t ev_done = nullptr;
   // device scene
   rt_node* d_nodes = nullptr;
   DMat* d_mats = nullptr;
@@ -748,6 +751,17 @@ int hip_fail(hipError_t e, const char* what) {
     hipError_t _e = (x);                           \
     if (_e != hipSuccess) return hip_fail(_e, #x); \
   } while (0)
+
+// Device allocation released when it goes out of scope (every return path of the blocking calls).
+struct DevBuf {
+  void* p = nullptr;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
 
 int invalid(const std::string& s) {
   rt::set_error(s);
@@ -807,7 +821,7 @@ struct Validator {
         case RT_NODE_BVH:
           if (!child_ok(i, x.a) || !child_ok(i, x.b)) return fail("BVH child must precede its parent");
           if (x.c <= 0) return fail("BVH size must be positive");
-          stack_need[i] = std::max(1 + stack_need[x.a], stack_need[x.b]);
+          stack_need[i] = rt::bvh_stack_need(x, stack_need[x.a], stack_need[x.b]);
           frame_depth[i] = std::max(frame_depth[x.a], frame_depth[x.b]);
           break;
         case RT_NODE_SPHERE:
@@ -907,7 +921,8 @@ int check_params(const rt_render_params* p) {
   if (p->rng_mode != RT_RNG_EXACT && p->rng_mode != RT_RNG_PHILOX) return invalid("unknown rng_mode");
   const int tile = p->tile ? p->tile : 16;
   if (tile <= 0 || tile % 8) return invalid("tile must be a positive multiple of 8");
-  if (p->shard_count < 0 || (p->shard_count > 0 && (p->shard_rank < 0 || p->shard_rank >= p->shard_count)))
+  if (p->shard_count < 0 || (p->shard_count > 0 && (p->shard_rank < 0 || p->shard_rank >= p->shard_count)) ||
+      (p->shard_count <= 1 && p->shard_rank != 0))
     return invalid("bad shard_rank/shard_count");
   if ((long long)p->width * p->height >= (1ll << 32)) return invalid("image too large for 32-bit pixel ids");
   return RT_OK;
@@ -1020,12 +1035,13 @@ unsigned scene_features(const rt_scene_desc* d) {
   return f;
 }
 
-int launch_combine(const RenderArgs& A, hipStream_t st) {
+int launch_combine(rt_ctx* c, const RenderArgs& A, hipStream_t st) {
   RenderArgs B = A;
   void* args[] = {&B};
   HIPCHK(hipLaunchKernel((const void*)combine_chunks, dim3((unsigned)((A.slab + 255) / 256)), dim3(256), args, 0,
                          st));
   HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev_done, st));
   return RT_OK;
 }
 
@@ -1058,10 +1074,13 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   A.work = d_work;
   A.out_rgb = d_rgb;
   A.out_lin = d_lin;
+  // The work counter and the chunk-sum buffer are the ctx's: order this launch after the previous
+  // one, whichever stream that was on.
+  HIPCHK(hipStreamWaitEvent(st, c->ev_done, 0));
   {  // chunk sums: [chunk][slab pixel][3] doubles, kept on the ctx and grown on demand
     const size_t need = (size_t)A.chunks * (size_t)slab * 3 * sizeof(double);
     if (need > c->partial_bytes) {
-      HIPCHK(hipStreamSynchronize(st));
+      HIPCHK(hipEventSynchronize(c->ev_done));
       (void)hipFree(c->d_partial);
       c->d_partial = nullptr;
       c->partial_bytes = 0;
@@ -1131,7 +1150,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
       HIPCHK(hipEventRecord(c->ev0, st));
       HIPCHK(hipLaunchKernel(fn, dim3(c->cu_count), dim3(block), args, bytes, st));
       HIPCHK(hipEventRecord(c->ev1, st));
-      return launch_combine(A, st);
+      return launch_combine(c, A, st);
     }
   }
   const void* fn = philox_kernel(var, loop, false, count ? 1 : waves, count);
@@ -1145,7 +1164,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   HIPCHK(hipLaunchKernel(fn, dim3(grid), dim3(RT_BLOCK), args, 0, st));
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev1, st));
-  return launch_combine(A, st);
+  return launch_combine(c, A, st);
 }
 
 }  // namespace
@@ -1160,22 +1179,32 @@ int rt_device_count(int* out) {
 
 int rt_create(int device, rt_ctx** out) {
   if (!out) return invalid("null out");
+  *out = nullptr;
   int n = 0;
   HIPCHK(hipGetDeviceCount(&n));
   if (device < 0 || device >= n) return invalid("device index out of range");
   HIPCHK(hipSetDevice(device));
   rt_ctx* c = new rt_ctx();
   c->device = device;
-  hipDeviceProp_t prop;
-  HIPCHK(hipGetDeviceProperties(&prop, device));
-  c->cu_count = prop.multiProcessorCount;
-  int bpc = 0;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void*)render_philox<F_ALL, 1>, RT_BLOCK, 0));
-  c->blocks_per_cu = bpc;
-  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  HIPCHK(hipEventCreate(&c->ev0));
-  HIPCHK(hipEventCreate(&c->ev1));
-  HIPCHK(hipMalloc((void**)&c->d_counter, 256));
+  auto init = [c]() -> int {
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, c->device));
+    c->cu_count = prop.multiProcessorCount;
+    int bpc = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void*)render_philox<F_ALL, 1>, RT_BLOCK, 0));
+    c->blocks_per_cu = bpc;
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&c->ev0));
+    HIPCHK(hipEventCreate(&c->ev1));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
+    HIPCHK(hipMalloc((void**)&c->d_counter, 256));
+    return RT_OK;
+  };
+  const int rc = init();
+  if (rc) {
+    rt_destroy(c);
+    return rc;
+  }
   *out = c;
   return RT_OK;
 }
@@ -1188,6 +1217,7 @@ void rt_destroy(rt_ctx* c) {
   (void)hipFree(c->d_partial);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->ev_done) (void)hipEventDestroy(c->ev_done);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1223,7 +1253,6 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
   dd.nodes = nodes.data();
   dd.n_nodes = (int)nodes.size();
   const rt_scene_desc* d = &dd;
-  c->rebuilt_bvh = dd.world_root != din->world_root;
   Validator v{d};
   if (!v.run()) {
     rt::set_error("rt_upload_scene: " + v.err);
@@ -1250,7 +1279,10 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
       return invalid("rt_upload_scene: material texture out of range");
     mats[i] = DMat{m.type, m.texture, m.param, m.type != RT_MAT_DIELECTRIC && tex_needs_uv(d, m.texture), 0};
   }
+  if (d->image_pool_bytes < 0 || (d->image_pool_bytes > 0 && !d->image_pool))
+    return invalid("rt_upload_scene: image_pool is null but image_pool_bytes > 0");
   free_scene(c);
+  c->rebuilt_bvh = dd.world_root != din->world_root;
   int rc;
   if ((rc = upload(&c->d_nodes, v.nodes.data(), v.nodes.size())) ||
       (rc = upload(&c->d_mats, mats.data(), mats.size())) ||
@@ -1380,41 +1412,38 @@ int rt_assemble_linear_async(rt_ctx* c, const rt_render_params* p, const double*
 int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, const uint64_t* col_gens, uint8_t* out_rgb,
               double* out_lin, uint64_t* out_gens) {
   if (!c || !cam || !pin || !out_rgb) return invalid("null argument");
-  int rc = check_params(pin);
+  rt_render_params p = *pin;  // whole image: the shard fields are ignored
+  p.shard_rank = 0;
+  p.shard_count = 1;
+  int rc = check_params(&p);
   if (rc) return rc;
   if (!c->has_scene) {
     rt::set_error("rt_render: no scene uploaded");
     return RT_E_STATE;
   }
+  if (p.rng_mode == RT_RNG_EXACT && !col_gens) return invalid("rt_render: tier A needs col_gens (2*width words)");
   HIPCHK(hipSetDevice(c->device));
-  rt_render_params p = *pin;
-  p.shard_rank = 0;
-  p.shard_count = 1;
   const long long npx = (long long)p.width * p.height;
   hipStream_t st = c->stream;
-  uint8_t* d_img = nullptr;
-  double* d_img_lin = nullptr;
-  HIPCHK(hipMalloc((void**)&d_img, (size_t)npx * 3));
-  if (out_lin) HIPCHK(hipMalloc((void**)&d_img_lin, sizeof(double) * (size_t)npx * 3));
-  int result = RT_OK;
+  DevBuf img, img_lin, slab_buf, slab_lin, gens;  // freed on every return path
+  HIPCHK(hipMalloc(&img.p, (size_t)npx * 3));
+  if (out_lin) HIPCHK(hipMalloc(&img_lin.p, sizeof(double) * (size_t)npx * 3));
+  uint8_t* d_img = (uint8_t*)img.p;
+  double* d_img_lin = (double*)img_lin.p;
   if (p.rng_mode == RT_RNG_PHILOX) {
     int tile, tiles_x;
     long long tt, ps, slab;
     geometry(&p, tile, tiles_x, tt, ps, slab);
-    uint8_t* d_slab = nullptr;
-    double* d_slab_lin = nullptr;
-    HIPCHK(hipMalloc((void**)&d_slab, (size_t)slab * 3));
-    if (out_lin) HIPCHK(hipMalloc((void**)&d_slab_lin, sizeof(double) * (size_t)slab * 3));
-    result = launch_philox(c, cam, &p, 0, 1, d_slab, d_slab_lin, st);
-    if (!result) result = rt_assemble_async(c, &p, d_slab, d_img, st);
-    if (!result && out_lin) result = rt_assemble_linear_async(c, &p, d_slab_lin, d_img_lin, st);
+    HIPCHK(hipMalloc(&slab_buf.p, (size_t)slab * 3));
+    if (out_lin) HIPCHK(hipMalloc(&slab_lin.p, sizeof(double) * (size_t)slab * 3));
+    rc = launch_philox(c, cam, &p, 0, 1, (uint8_t*)slab_buf.p, (double*)slab_lin.p, st);
+    if (!rc) rc = rt_assemble_async(c, &p, (const uint8_t*)slab_buf.p, d_img, st);
+    if (!rc && out_lin) rc = rt_assemble_linear_async(c, &p, (const double*)slab_lin.p, d_img_lin, st);
     HIPCHK(hipStreamSynchronize(st));
-    (void)hipFree(d_slab);
-    (void)hipFree(d_slab_lin);
+    if (rc) return rc;
   } else {
-    if (!col_gens) return invalid("rt_render: tier A needs col_gens (2*width words)");
-    uint64_t* d_gens = nullptr;
-    HIPCHK(hipMalloc((void**)&d_gens, sizeof(uint64_t) * 2 * (size_t)p.width));
+    HIPCHK(hipMalloc(&gens.p, sizeof(uint64_t) * 2 * (size_t)p.width));
+    uint64_t* d_gens = (uint64_t*)gens.p;
     HIPCHK(hipMemcpyAsync(d_gens, col_gens, sizeof(uint64_t) * 2 * (size_t)p.width, hipMemcpyHostToDevice, st));
     RenderArgs A{};
     A.S = c->scene;
@@ -1434,13 +1463,9 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, cons
     if (out_gens)
       HIPCHK(hipMemcpyAsync(out_gens, d_gens, sizeof(uint64_t) * 2 * (size_t)p.width, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    (void)hipFree(d_gens);
   }
-  if (result) return result;
   HIPCHK(hipMemcpy(out_rgb, d_img, (size_t)npx * 3, hipMemcpyDeviceToHost));
   if (out_lin) HIPCHK(hipMemcpy(out_lin, d_img_lin, sizeof(double) * (size_t)npx * 3, hipMemcpyDeviceToHost));
-  (void)hipFree(d_img);
-  (void)hipFree(d_img_lin);
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
   c->last_ms = ms;
@@ -1462,21 +1487,18 @@ int rt_render_work(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin,
   int tile, tiles_x;
   long long tt, ps, slab;
   geometry(&p, tile, tiles_x, tt, ps, slab);
-  uint8_t* d_slab = nullptr;
-  unsigned long long* d_work = nullptr;
-  HIPCHK(hipMalloc((void**)&d_slab, (size_t)slab * 3));
-  HIPCHK(hipMalloc((void**)&d_work, sizeof(unsigned long long) * 16));
+  DevBuf slab_buf, work;
+  HIPCHK(hipMalloc(&slab_buf.p, (size_t)slab * 3));
+  HIPCHK(hipMalloc(&work.p, sizeof(unsigned long long) * 16));
+  unsigned long long* d_work = (unsigned long long*)work.p;
   HIPCHK(hipMemsetAsync(d_work, 0, sizeof(unsigned long long) * 16, c->stream));
-  rc = launch_philox(c, cam, &p, p.shard_rank, shards, d_slab, nullptr, c->stream, d_work);
-  if (!rc) {
-    HIPCHK(hipStreamSynchronize(c->stream));
-    unsigned long long w[16];
-    HIPCHK(hipMemcpy(w, d_work, sizeof w, hipMemcpyDeviceToHost));
-    for (int i = 0; i < 16; ++i) out_work[i] = w[i];
-  }
-  (void)hipFree(d_slab);
-  (void)hipFree(d_work);
-  return rc;
+  rc = launch_philox(c, cam, &p, p.shard_rank, shards, (uint8_t*)slab_buf.p, nullptr, c->stream, d_work);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (rc) return rc;
+  unsigned long long w[16];
+  HIPCHK(hipMemcpy(w, d_work, sizeof w, hipMemcpyDeviceToHost));
+  for (int i = 0; i < 16; ++i) out_work[i] = w[i];
+  return RT_OK;
 }
 
 int rt_last_kernel_ms(rt_ctx* c, double* out_ms) {
@@ -1502,9 +1524,11 @@ int rt_debug_closest_hits(rt_ctx* c, const double* rays, int n, double tmin, dou
     return unsupported("rt_debug_closest_hits: no 4-wide tree for this world");
   if (n == 0) return RT_OK;
   HIPCHK(hipSetDevice(c->device));
-  double *d_rays = nullptr, *d_out = nullptr;
-  HIPCHK(hipMalloc((void**)&d_rays, sizeof(double) * 7 * (size_t)n));
-  HIPCHK(hipMalloc((void**)&d_out, sizeof(double) * 12 * (size_t)n));
+  DevBuf rays_buf, out_buf;
+  HIPCHK(hipMalloc(&rays_buf.p, sizeof(double) * 7 * (size_t)n));
+  HIPCHK(hipMalloc(&out_buf.p, sizeof(double) * 12 * (size_t)n));
+  double* d_rays = (double*)rays_buf.p;
+  double* d_out = (double*)out_buf.p;
   HIPCHK(hipMemcpy(d_rays, rays, sizeof(double) * 7 * (size_t)n, hipMemcpyHostToDevice));
   const int joint = !(flags & RT_FLAG_REFERENCE_CULL);
   const dim3 grid((n + RT_BLOCK - 1) / RT_BLOCK);
@@ -1517,8 +1541,6 @@ int rt_debug_closest_hits(rt_ctx* c, const double* rays, int n, double tmin, dou
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipMemcpy(out, d_out, sizeof(double) * 12 * (size_t)n, hipMemcpyDeviceToHost));
-  (void)hipFree(d_rays);
-  (void)hipFree(d_out);
   return RT_OK;
 }
 
@@ -1526,20 +1548,18 @@ int rt_debug_math(rt_ctx* c, int op, const double* x, const double* y, int n, do
   if (!c || !x || !y || !out || n < 0 || op < 0 || op > 11) return invalid("rt_debug_math: bad argument");
   if (n == 0) return RT_OK;
   HIPCHK(hipSetDevice(c->device));
-  double *dx = nullptr, *dy = nullptr, *dout = nullptr;
   const size_t bytes = sizeof(double) * (size_t)n;
-  HIPCHK(hipMalloc((void**)&dx, bytes));
-  HIPCHK(hipMalloc((void**)&dy, bytes));
-  HIPCHK(hipMalloc((void**)&dout, bytes));
+  DevBuf bx, by, bout;
+  HIPCHK(hipMalloc(&bx.p, bytes));
+  HIPCHK(hipMalloc(&by.p, bytes));
+  HIPCHK(hipMalloc(&bout.p, bytes));
+  double *dx = (double*)bx.p, *dy = (double*)by.p, *dout = (double*)bout.p;
   HIPCHK(hipMemcpy(dx, x, bytes, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(dy, y, bytes, hipMemcpyHostToDevice));
   hipLaunchKernelGGL(math_probe, dim3((n + 255) / 256), dim3(256), 0, c->stream, op, dx, dy, n, dout);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost));
-  (void)hipFree(dx);
-  (void)hipFree(dy);
-  (void)hipFree(dout);
   return RT_OK;
 }
 

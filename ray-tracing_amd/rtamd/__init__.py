@@ -108,7 +108,7 @@ EXPORTED = [
     "rt_device_count", "rt_create", "rt_destroy", "rt_upload_scene", "rt_render", "rt_shard_geometry",
     "rt_render_shard_async", "rt_assemble_async", "rt_assemble_linear_async", "rt_last_kernel_ms",
     "rt_debug_closest_hits", "rt_debug_math", "rt_render_work", "rt_upload_scene_ex", "rt_rebuild_bvh",
-    "rt_wide_bvh",
+    "rt_wide_bvh", "rt_tree_stack_need",
 ]
 
 # include/rt_wide.h: one 4-wide node (128 B)
@@ -183,6 +183,7 @@ def lib() -> C.CDLL:
             "rt_upload_scene_ex": (I, [C.c_void_p, P(rt_scene_desc), C.c_uint32]),
             "rt_rebuild_bvh": (I, [P(rt_scene_desc), P(rt_node), I, P(I), P(I)]),
             "rt_wide_bvh": (I, [P(rt_node), I, I, C.c_void_p, I, P(I), P(I)]),
+            "rt_tree_stack_need": (I, [P(rt_node), I, I, P(I)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -369,6 +370,15 @@ def wide_bvh(scene: Scene, root: Optional[int] = None) -> Tuple[np.ndarray, int]
     _check(lib().rt_wide_bvh(scene.desc.nodes, scene.desc.n_nodes, r, out.ctypes.data_as(C.c_void_p), n.value,
                              C.byref(n), C.byref(need)), "rt_wide_bvh")
     return out, need.value
+
+
+def tree_stack_need(scene: Scene, root: Optional[int] = None) -> int:
+    """rt_tree_stack_need: the binary walk's stack bound (entries) for the tree at `root`
+    (default: the scene's world root), as rt_upload_scene sizes the LDS stacks."""
+    need = C.c_int(0)
+    r = scene.desc.world_root if root is None else root
+    _check(lib().rt_tree_stack_need(scene.desc.nodes, scene.desc.n_nodes, r, C.byref(need)), "rt_tree_stack_need")
+    return need.value
 
 
 def make_scene(name: str, gen: Tuple[int, int], t0: float = 0.0, t1: float = 1.0,

@@ -45,6 +45,9 @@ def test_param_validation_without_gpu():
         rtamd.shard_geometry(rtamd.make_params(10, 10, 1, 1, tile=12))
     with pytest.raises(rtamd.RTError):
         rtamd.shard_geometry(rtamd.make_params(10, 10, 1, 1, shard_rank=2, shard_count=2))
+    for count in (0, 1):  # an unsharded launch has only rank 0 (a stray rank shifted the tile map)
+        with pytest.raises(rtamd.RTError):
+            rtamd.shard_geometry(rtamd.make_params(10, 10, 1, 1, shard_rank=1, shard_count=count))
     tt, per, slab = rtamd.shard_geometry(rtamd.make_params(1200, 800, 1, 1, tile=16, shard_count=8))
     assert tt == 75 * 50 and per == (3750 + 7) // 8 and slab == per * 256
 

@@ -126,3 +126,82 @@ def test_wide_tree_covers_leaves_and_contains_boxes(name, param):
         return [i]
     assert sorted(seen) == sorted(bin_leaves(rb.desc.world_root))
     print(f"{name}: {len(set(seen))} leaves, {len(wide)} wide nodes, stack bound {need}")
+
+
+def _spine_scene(n=45):
+    """Skewed world: n unit spheres in a row at x = -2^k. The SAH rebuild's centroid bins put all
+    but the far sphere in bin 0 at every level, so the rebuilt tree is a deep spine."""
+    b = rtamd.Builder(rtamd.randGen(1024))
+    mat = b.lambertian(b.constantColor(0.3, 0.6, 0.2))
+    ids = [b.sphere((-(2.0 ** k), 0.0, 0.0), 0.5, mat) for k in range(n)]
+    world = b.makeBVH((0.0, 1.0), ids)
+    return b.finish(world, -1, (0.7, 0.8, 0.9))
+
+
+def _walk_need(nodes, node, signs, memo):
+    """Deepest stack the walk (rt_trace.h traverse / walk_step) reaches below `node` for a ray
+    whose direction has the given component signs, every box accepted (the worst case)."""
+    key = node
+    if key in memo:
+        return memo[key]
+    nd = nodes[node]
+    t = int(nd["type"])
+    if t == rtamd.RT_NODE_BVH:
+        c = int(nd["c"])
+        flip = (c & rtamd.RT_BVH_ORDERED) != 0 and signs[c & 3] < 0
+        first, second = (int(nd["b"]), int(nd["a"])) if flip else (int(nd["a"]), int(nd["b"]))
+        r = max(1 + _walk_need(nodes, first, signs, memo), _walk_need(nodes, second, signs, memo))
+    elif t in (rtamd.RT_NODE_TRANSLATE, rtamd.RT_NODE_ROTATE):
+        inner = _walk_need(nodes, int(nd["a"]), signs, memo)
+        chain = _is_chain(nodes, int(nd["a"]))
+        r = 0 if chain else 1 + inner
+    else:
+        r = 0
+    memo[key] = r
+    return r
+
+
+def _is_chain(nodes, i):
+    t = int(nodes[i]["type"])
+    if t in (rtamd.RT_NODE_TRANSLATE, rtamd.RT_NODE_ROTATE):
+        return _is_chain(nodes, int(nodes[i]["a"]))
+    return t in (rtamd.RT_NODE_SPHERE, rtamd.RT_NODE_MOVING_SPHERE, rtamd.RT_NODE_RECT_XY, rtamd.RT_NODE_RECT_XZ,
+                 rtamd.RT_NODE_RECT_YZ, rtamd.RT_NODE_CUBOID)
+
+
+def _left_first_bound(nodes, node, memo):
+    """The bound the validator used before ordered nodes were accounted for."""
+    if node in memo:
+        return memo[node]
+    nd = nodes[node]
+    r = 0
+    if int(nd["type"]) == rtamd.RT_NODE_BVH:
+        r = max(1 + _left_first_bound(nodes, int(nd["a"]), memo), _left_first_bound(nodes, int(nd["b"]), memo))
+    memo[node] = r
+    return r
+
+
+@pytest.mark.parametrize("name,param", [("random_book_one", 0), ("stress_spheres", 2000), ("stress_spheres", 20000),
+                                        ("random", 0), ("cornell", 0), ("next_week_final", 0), ("spine", 0)])
+def test_stack_bound_covers_every_ray_direction(name, param):
+    """rt_tree_stack_need (the bound rt_upload_scene sizes the LDS stacks with) is at least the
+    deepest stack the walk reaches over all 8 direction-sign combinations, on the tree the device
+    walks (the SAH rebuild where it applies) and on the caller's tree (the tie redo walk)."""
+    import itertools
+    if name == "spine":
+        scene = _spine_scene()
+    else:
+        scene, _ = rtamd.make_scene(name, rtamd.randGen(1024), param=param)
+    rb = rtamd.rebuilt_scene(scene)
+    for sc in (rb, scene):
+        nodes = sc.nodes
+        bound = rtamd.tree_stack_need(sc)
+        worst = max(_walk_need(nodes, sc.desc.world_root, s, {}) for s in itertools.product((1, -1), repeat=3))
+        assert worst <= bound, (name, worst, bound)
+        assert bound <= 30  # RT_STACK - 2: upload admits it
+    if name == "spine":
+        # the rebuilt spine is where left-first accounting fell short
+        nodes = rb.nodes
+        worst = max(_walk_need(nodes, rb.desc.world_root, s, {}) for s in itertools.product((1, -1), repeat=3))
+        assert rb.desc.world_root != scene.desc.world_root
+        assert _left_first_bound(nodes, rb.desc.world_root, {}) < worst

@@ -293,3 +293,18 @@ def test_cornell_1000spp_tracks_reference_render(gpu_ctx):
     # measured (round 1): image means within 0.013 levels, block |d| mean 0.34, p99 1.47, max 2.9
     assert np.abs(rgb.reshape(-1, 3).mean(0) - ref["image_mean"]).max() < 0.1
     assert d.mean() < 0.5 and np.percentile(d, 99) < 2.5 and d.max() < 5.0
+
+
+@pytest.mark.parametrize("wide", ["0", "1"])
+def test_skewed_spine_world_walks(gpu_ctx, wide, monkeypatch):
+    """A world whose SAH rebuild is a deep spine (45 spheres at x = -2^k): rays along the row
+    enter the near child at every level with the far one stacked, so the binary walk's LDS stack
+    must be sized for 1 + max(child needs) on rebuilt nodes (rt_tree_stack_need). Images from
+    the binary (RTAMD_WIDE=0) and 4-wide walks match the oracle."""
+    from test_bvh import _spine_scene
+    sc = _spine_scene()
+    assert rtamd.tree_stack_need(rtamd.rebuilt_scene(sc)) >= 10
+    cam = rtamd.newCamera((10.0, 0.05, 0.02), (-1.0, 0.0, 0.0), (0.0, 1.0, 0.0), 8.0, 1.0, 0.0, 10.0, 0.0, 1.0)
+    p = rtamd.make_params(48, 48, 4, 8, rtamd.RT_RNG_PHILOX, seed=21)
+    monkeypatch.setenv("RTAMD_WIDE", wide)
+    _cmp(gpu_ctx, sc, cam, p)

@@ -3,6 +3,7 @@ surface) that exercise the device path's structural limits — instance frames n
 beyond RT_MAX_FRAMES (replacement loop vs per-sample loop), media inside frames — and the
 upload's validation of malformed descriptors (error codes, no fallback)."""
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -98,3 +99,47 @@ def test_upload_rejects_malformed_scenes(gpu_ctx):
     assert rc == rtamd.RT_E_UNSUPPORTED, rc
     after, _, _ = gpu_ctx.render(cam, p)
     assert np.array_equal(before, after)
+
+
+def test_upload_rejects_null_image_pool_and_keeps_scene(gpu_ctx):
+    """image_pool_bytes > 0 with a null pool is refused (the device would read textures through a
+    null pointer); the previously uploaded scene stays usable."""
+    import ctypes as C
+    sc, _ = rtamd.make_scene("three_spheres", rtamd.randGen(1024))
+    gpu_ctx.upload(sc)
+    cam = rtamd.camera("random_scene", 32, 16)
+    p = rtamd.make_params(32, 16, 2, 5, rtamd.RT_RNG_PHILOX, seed=1)
+    before, _, _ = gpu_ctx.render(cam, p)
+    earth = np.load(os.path.join(os.path.dirname(__file__), "golden", "earthmap_rgb8.npz"))["rgb"]
+    bad, _ = rtamd.make_scene("earth", rtamd.randGen(1024), earth=earth)
+    d = rtamd.rt_scene_desc()
+    C.pointer(d)[0] = bad.desc
+    d.image_pool = C.POINTER(C.c_uint8)()
+    rc = rtamd.lib().rt_upload_scene(gpu_ctx._h, C.byref(d))
+    assert rc == rtamd.RT_E_INVALID and b"image_pool" in rtamd.lib().rt_last_error()
+    after, _, _ = gpu_ctx.render(cam, p)
+    assert np.array_equal(before, after)
+
+
+def test_launches_on_two_streams_are_ordered(gpu_ctx):
+    """Shard launches on two different streams share the ctx's work counter and chunk-sum buffer:
+    the second waits for the first, so both slabs equal their one-stream renders."""
+    import torch
+    sc, _ = rtamd.make_scene("random_book_one", rtamd.randGen(1024))
+    gpu_ctx.upload(sc)
+    cam = rtamd.camera("random_scene", 96, 64)
+    ps = [rtamd.make_params(96, 64, 40, 20, rtamd.RT_RNG_PHILOX, seed=s, shard_rank=0, shard_count=1) for s in (3, 4)]
+    _, _, slab = rtamd.shard_geometry(ps[0])
+    ref = []
+    for p in ps:
+        buf = torch.zeros((slab, 3), dtype=torch.uint8, device="cuda")
+        gpu_ctx.render_shard_async(cam, p, buf.data_ptr())
+        torch.cuda.synchronize()
+        ref.append(buf.cpu().numpy())
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    bufs = [torch.zeros((slab, 3), dtype=torch.uint8, device="cuda") for _ in ps]
+    for p, b, st in zip(ps, bufs, streams):
+        gpu_ctx.render_shard_async(cam, p, b.data_ptr(), stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    for b, r in zip(bufs, ref):
+        assert np.array_equal(b.cpu().numpy(), r)
