@@ -265,7 +265,7 @@ def main():
             n = max(1, work["samples"])
             out["phase_split"] = {k: round(v, 4) for k, v in work.pop("phase_split").items()}
             slots = work.pop("lane_slots")
-            leaf_hits, pretest_drops = work.pop("leaf_hits"), work.pop("leaf_pretest_drops")
+            leaf_hits = work.pop("leaf_hits")
             if slots["outer_iterations"]:  # lane utilisation of the replacement loop's phases
                 out["lane_utilisation"] = {
                     "wide_steps": round(work["wide_nodes"] / max(1, slots["wide_steps"]), 4),
@@ -295,7 +295,6 @@ def main():
                            "frac": round(fl32 / FP32_PEAK_TFLOPS, 5), "flops_per_sample": round(f32, 1)}
             out["work_per_sample"] = {k: round(v, 3) for k, v in per.items() if k != "samples"}
             out["work_per_sample"]["leaf_hits"] = round(leaf_hits / n, 3)
-            out["work_per_sample"]["leaf_pretest_drops"] = round(pretest_drops / n, 3)
             if counters:
                 out["work_per_sample_reference_cull"] = {k: round(v / max(1, counters["samples"]), 3)
                                                          for k, v in counters.items() if k != "samples"}

@@ -363,8 +363,7 @@ int rt_assemble_linear_async(rt_ctx* ctx, const rt_render_params* p, const doubl
  * for this shard; out_work[8..10] = wave time (s_memtime ticks, summed over waves) spent acquiring work and
  * starting samples / traversing / shading; out_work[11..13] (ray-replacement loop only) = live-lane
  * slots of 4-wide node steps, of leaf steps and of outer iterations (lane utilisation = work / slots);
- * out_work[14] = leaf tests that found a hit, out_work[15] = sphere leaves the 4-wide walk's fp32
- * pretest dropped before testing them (RTAMD_PRETEST=0 disables the pretest).
+ * out_work[14] = leaf tests that found a hit (replacement loop); the rest 0.
  */
 int rt_render_work(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* p, uint64_t out_work[16]);
 

@@ -139,7 +139,6 @@ struct Scene {
   int lights;
   int ref_walk;   // media or instance frames: the replacement loop walks the caller's tree in the
                   // reference's own order (media draw order, Lib.hs:971-988,1053-1080)
-  int pretest;    // 4-wide walk over spheres: conservative fp32 miss test before a leaf is parked
   double bg[3];
 };
 

@@ -515,7 +515,6 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     wave_add(&A.work[12], cnt.lslot);
     wave_add(&A.work[13], cnt.oslot);
     wave_add(&A.work[14], cnt.phit);
-    wave_add(&A.work[15], cnt.prej);
     if ((threadIdx.x & 63) == 0) {
       atomicAdd(&A.work[8], ph_setup);
       atomicAdd(&A.work[9], ph_trav);
@@ -1098,9 +1097,6 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   // (the full variant's walks over the caller's tree: 16, C4 1496 vs 1567 ms at 200 spp)
   A.trav_stop = stop_env ? std::max(0, std::min(63, std::atoi(stop_env)))
                          : (c->n_nodes > 20000 || variant_for(c->features) == F_ALL ? 16 : 8);
-  // fp32 sphere pretest before a leaf is parked (4-wide walk, spheres-only worlds; RTAMD_PRETEST=0
-  // disables it)
-  A.S.pretest = !env_off("RTAMD_PRETEST");
   const char* leaf_env = std::getenv("RTAMD_LEAF_STOP");
   // leaf steps once <= that many lanes still seek their first leaf (measured: C2 212.6 ms at 6-8/64
   // vs 219.7 at 0 and 232 without postponement; C5 (16 spp) 219.9 ms at 16/64 vs 326 at 0)
@@ -1318,7 +1314,6 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
   const bool frames = v.frame_depth[d->world_root] > 0;
   c->replace_ok = v.frame_depth[d->world_root] <= RT_MAX_FRAMES;
   S.ref_walk = (c->features & F_MEDIA) || frames;
-  S.pretest = 0;  // set per launch
   if (frames) c->features |= F_FRAMES;
   if (c->replace_ok && !S.ref_walk) {  // 4-wide fp32-box tree over the same world tree (unflagged node copy)
     std::vector<rt_wnode> wide;
@@ -1538,12 +1533,7 @@ int rt_debug_closest_hits(rt_ctx* c, const double* rays, int n, double tmin, dou
   HIPCHK(hipMemcpy(d_rays, rays, sizeof(double) * 7 * (size_t)n, hipMemcpyHostToDevice));
   const int joint = !(flags & RT_FLAG_REFERENCE_CULL);
   const dim3 grid((n + RT_BLOCK - 1) / RT_BLOCK);
-  Scene S = c->scene;
-  S.pretest = !env_off("RTAMD_PRETEST");
-  if ((flags & RT_DEBUG_WIDE) && variant_for(c->features) == kVarSpheres)  // the render's spheres walk (pretest)
-    hipLaunchKernelGGL(closest_hits<F_UV | F_WIDE>, grid, dim3(RT_BLOCK), 0, c->stream, S, d_rays, n, tmin, tmax,
-                       seed, joint, 1, d_out);
-  else if (flags & RT_DEBUG_WIDE)
+  if (flags & RT_DEBUG_WIDE)
     hipLaunchKernelGGL(closest_hits<F_ALL | F_UV | F_WIDE>, grid, dim3(RT_BLOCK), 0, c->stream, c->scene, d_rays, n,
                        tmin, tmax, seed, joint, 1, d_out);
   else

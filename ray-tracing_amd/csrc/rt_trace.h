@@ -23,7 +23,7 @@ enum : unsigned {
 struct Cnt {
   unsigned box, prim, other, light, wide;
   unsigned islot, lslot, oslot;  // lane slots (live lanes) of wide-node steps, leaf steps, outer iterations
-  unsigned phit, prej;           // leaf tests that found a hit; leaves the fp32 sphere pretest dropped
+  unsigned phit;                 // leaf tests that found a hit
 };
 
 // ------------------------------------------------------------------ textures (Lib.hs:441-513)
@@ -824,52 +824,8 @@ constexpr int kNone = (int)0x80000000;  // Trav::node: nothing left but the post
 __device__ __forceinline__ int trav_pop(Trav& t, const int* stk, int stride) {
   return t.sp ? stk[(--t.sp) * stride] : kNone;
 }
-// Conservative fp32 miss test of a sphere leaf (centre c, radius r) against the walk's ray. The
-// fp64 test (sphere_t) needs disc = b^2 - a*c > 0, and disc = r^2 |d|^2 - |oc x d|^2 (Lagrange's
-// identity), so it can only accept when |oc x d| < r |d| up to its own rounding (~2^-50 relative).
-// In fp32, oc = o32 - c32 and d32 carry relative errors of a few 2^-24 each, so every component of
-// the computed cross product is within 12 * 2^-24 * M of the exact one, M = (|c|inf + |o|inf)
-// |d|inf, and its norm within E = 2^-18 M (4x over). The leaf is dropped only when
-// |cross32|^2 (1 - 2^-18) > ((r32 |d32|)(1 + 2^-18) + E)^2 (1 + 2^-18), every term finite: then
-// |oc x d| > r |d| by far more than either side's rounding, and the fp64 test would miss too.
-// Rays the fp32 walk cannot describe (slack = inf) keep every leaf.
-__device__ __forceinline__ bool sphere_may_hit32(const Trav& t, const rt_node* n) {
-  const float cx = (float)n->f[0], cy = (float)n->f[1], cz = (float)n->f[2];
-  const float r = (float)n->f[3] * (1.0f + 0x1p-22f);
-  const float dx = (float)t.ray.d.x, dy = (float)t.ray.d.y, dz = (float)t.ray.d.z;
-  const float ox = t.o32x - cx, oy = t.o32y - cy, oz = t.o32z - cz;
-  const float crx = oy * dz - oz * dy, cry = oz * dx - ox * dz, crz = ox * dy - oy * dx;
-  const float x2 = crx * crx + cry * cry + crz * crz;
-  const float d2 = dx * dx + dy * dy + dz * dz;
-  const float cm = fmaxf(fmaxf(fabsf(cx), fabsf(cy)), fabsf(cz));
-  const float om = fmaxf(fmaxf(fabsf(t.o32x), fabsf(t.o32y)), fabsf(t.o32z));
-  const float dm = fmaxf(fmaxf(fabsf(dx), fabsf(dy)), fabsf(dz));
-  const float e = (cm + om) * dm * 0x1p-18f;
-  const float rd = r * __fsqrt_rn(d2) * (1.0f + 0x1p-18f) + e;
-  const float rhs = rd * rd * (1.0f + 0x1p-18f);
-  const bool finite = (x2 < INFINITY) & (rhs < INFINITY) & (t.slack < INFINITY);
-  return !(finite & (x2 * (1.0f - 0x1p-18f) > rhs));
-}
-
-// node -> pend when node is a leaf and the slot is free, then continue with the next stack entry.
-// Spheres-only worlds (S.pretest): a leaf the fp32 test shows missed is dropped instead, so fewer
-// lanes hold a leaf and the wave runs fewer fp64 leaf steps.
-template <unsigned F>
-__device__ __forceinline__ void trav_postpone(const Scene& S, Trav& t, const int* stk, int stride, Cnt& cnt) {
-  if constexpr ((F & (F_RECT | F_MOVING | F_INST | F_MEDIA)) == 0) {
-    if (S.pretest) {
-      while (t.node < 0 && t.node != kNone && t.pend < 0) {
-        const int slot = ~t.node;
-        t.node = trav_pop(t, stk, stride);
-        if (sphere_may_hit32(t, &S.leaves[slot])) {
-          t.pend = slot;
-        } else if constexpr ((F & F_COUNT) != 0) {
-          ++cnt.prej;
-        }
-      }
-      return;
-    }
-  }
+// node -> pend when node is a leaf and the slot is free, then continue with the next stack entry
+__device__ __forceinline__ void trav_postpone(Trav& t, const int* stk, int stride) {
   if (t.node < 0 && t.node != kNone && t.pend < 0) {
     t.pend = ~t.node;
     t.node = trav_pop(t, stk, stride);
@@ -879,7 +835,7 @@ template <unsigned F>
 __device__ __forceinline__ void wide_inner(const Scene& S, Trav& t, int* stk, int stride, Cnt& cnt) {
   if constexpr ((F & F_COUNT) != 0) ++cnt.wide;
   if (!wide_node(S, t, stk, stride)) t.node = trav_pop(t, stk, stride);
-  trav_postpone<F>(S, t, stk, stride, cnt);
+  trav_postpone(t, stk, stride);
 }
 template <unsigned F, class R>
 __device__ __forceinline__ void wide_leaf(const Scene& S, Trav& t, double t_min, int* stk, int stride, Cnt& cnt, R& g,
@@ -889,7 +845,7 @@ __device__ __forceinline__ void wide_leaf(const Scene& S, Trav& t, double t_min,
     trav_leaf<F>(S, t, n, n->c, t_min, cnt, g, side);
     t.pend = -1;
   }
-  trav_postpone<F>(S, t, stk, stride, cnt);
+  trav_postpone(t, stk, stride);
 }
 
 // Step the wave's walking lanes until at most `stop` of them still walk (`walking` goes false when

@@ -516,9 +516,7 @@ class Context:
         out["phase_split"] = {"acquire_camera": int(w[8]) / tot, "traverse": int(w[9]) / tot, "shade": int(w[10]) / tot}
         # replacement loop only: live-lane slots of 4-wide node steps, leaf steps and outer iterations
         out["lane_slots"] = {"wide_steps": int(w[11]), "leaf_steps": int(w[12]), "outer_iterations": int(w[13])}
-        # replacement loop only: leaf tests that found a hit, leaves dropped by the fp32 sphere pretest
-        out["leaf_hits"] = int(w[14])
-        out["leaf_pretest_drops"] = int(w[15])
+        out["leaf_hits"] = int(w[14])  # replacement loop only: leaf tests that found a hit
         return out
 
     def last_kernel_ms(self) -> float:

@@ -309,19 +309,3 @@ def test_skewed_spine_world_walks(gpu_ctx, wide, monkeypatch):
     monkeypatch.setenv("RTAMD_WIDE", wide)
     _cmp(gpu_ctx, sc, cam, p)
 
-
-@pytest.mark.parametrize("name,param", [("random_book_one", 0), ("stress_spheres", 3000)])
-def test_sphere_pretest_is_output_identical(gpu_ctx, name, param, monkeypatch):
-    """The 4-wide walk's fp32 sphere pretest only drops leaves the fp64 test would miss: tier-B
-    images with and without it are identical in bytes and linear averages."""
-    sc, _ = _scene(name, param=param)
-    c = rtamd.camera("random_scene", 200, 120)
-    gpu_ctx.upload(sc)
-    p = rtamd.make_params(200, 120, 6, 50, rtamd.RT_RNG_PHILOX, seed=13)
-    monkeypatch.setenv("RTAMD_PRETEST", "1")
-    a, la, _ = gpu_ctx.render(c, p, linear=True)
-    w = gpu_ctx.render_work(c, p)
-    monkeypatch.setenv("RTAMD_PRETEST", "0")
-    b, lb, _ = gpu_ctx.render(c, p, linear=True)
-    assert np.array_equal(a, b) and np.array_equal(la, lb, equal_nan=True)
-    assert w["leaf_pretest_drops"] > 0
