@@ -539,7 +539,10 @@ __global__ void __launch_bounds__(RT_BLOCK, WAVES) render_philox2(RenderArgs A) 
 // LDS-staged replacement loop: the traversal's node array (the wide records for F_WIDE, else the
 // flat nodes) and the per-lane stacks live in the CU's LDS; leaves are read from global memory
 // under F_WIDE.
-template <unsigned F, int WAVES>
+// LEAF_LDS: the 4-wide walk's leaf table is staged too (n_leaves > 0); as its own instantiation,
+// so that the leaf reads compile to ds_read (a pointer that is LDS or global at run time would
+// make them flat loads, which wait on both the vector-memory and LDS counters).
+template <unsigned F, int WAVES, bool LEAF_LDS = false>
 __global__ void __launch_bounds__(WAVES * 256, WAVES)
     render_philox2_lds(RenderArgs A, int n_nodes, int stack_entries, int n_leaves) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -560,7 +563,8 @@ __global__ void __launch_bounds__(WAVES * 256, WAVES)
   Scene S = A.S;
   if constexpr ((F & F_WIDE) != 0) S.wnodes = reinterpret_cast<const rt_wnode*>(lds);
   else S.nodes = reinterpret_cast<const rt_node*>(lds);
-  if (n_leaves > 0) S.leaves = reinterpret_cast<const rt_node*>(lds + (size_t)n_nodes * rec);
+  if constexpr (LEAF_LDS) S.leaves = reinterpret_cast<const rt_node*>(lds + (size_t)n_nodes * rec);
+  else n_leaves = 0;
   int* stk = reinterpret_cast<int*>(lds + (size_t)n_nodes * rec + (size_t)n_leaves * sizeof(rt_node)) + threadIdx.x;
   // (the host sizes the dynamic LDS for stack_entries stack ints + kSideInts Side ints per lane
   // when F has F_FRAMES)
@@ -959,7 +963,14 @@ int waves_target(int dflt) {
 // sample per lane walk, 1 = ray replacement over the binary tree, 2 = replacement over the
 // 4-wide tree.
 template <unsigned V>
-const void* pick_w(bool lds, int w) {
+const void* pick_w(bool lds, int w, bool leaf_lds = false) {
+  if constexpr ((V & F_WIDE) != 0) {
+    if (lds && leaf_lds) {
+      if (w == 4) return (const void*)render_philox2_lds<V, 4, true>;
+      if (w == 2) return (const void*)render_philox2_lds<V, 2, true>;
+      if (w == 3) return (const void*)render_philox2_lds<V, 3, true>;
+    }  // (1 wave: the leaves are read from global memory)
+  }
   if (lds) {
     if (w == 2) return (const void*)render_philox2_lds<V, 2>;
     if (w == 4) return (const void*)render_philox2_lds<V, 4>;
@@ -972,12 +983,12 @@ const void* pick_w(bool lds, int w) {
   return (const void*)render_philox2<V, 1>;
 }
 template <unsigned V>
-const void* pick(int loop, bool lds, int w, bool count) {
+const void* pick(int loop, bool lds, int w, bool count, bool leaf_lds) {
   if (count) {
     if (loop == 2) return (const void*)render_philox2<V | F_WIDE | F_COUNT, 1>;
     return loop ? (const void*)render_philox2<V | F_COUNT, 1> : (const void*)render_philox<V | F_COUNT, 1>;
   }
-  if (loop == 2) return pick_w<V | F_WIDE>(lds, w);
+  if (loop == 2) return pick_w<V | F_WIDE>(lds, w, leaf_lds);
   if (loop == 1) return pick_w<V>(lds, w);
   if (lds) {
     if (w == 2) return (const void*)render_philox_lds<V, 2>;
@@ -990,9 +1001,9 @@ const void* pick(int loop, bool lds, int w, bool count) {
   if (w == 4) return (const void*)render_philox<V, 4>;
   return (const void*)render_philox<V, 1>;
 }
-const void* philox_kernel(unsigned var, int loop, bool lds, int w, bool count) {
-  if (var == kVarSpheres) return pick<kVarSpheres>(loop, lds, w, count);
-  if (var == kVarCornell) return pick<kVarCornell>(loop, lds, w, count);
+const void* philox_kernel(unsigned var, int loop, bool lds, int w, bool count, bool leaf_lds = false) {
+  if (var == kVarSpheres) return pick<kVarSpheres>(loop, lds, w, count, leaf_lds);
+  if (var == kVarCornell) return pick<kVarCornell>(loop, lds, w, count, leaf_lds);
   // full variant (media, frames, textures, motion): ray replacement over the caller's tree in the
   // reference's order (loop 1), or the per-sample loop (loop 0)
   if (count)
@@ -1144,7 +1155,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
     const int block = waves * 256;
     const size_t bytes = lds_bytes(waves, n_leaves);
     if (bytes <= 160 * 1024) {
-      const void* fn = philox_kernel(var, loop, true, waves, false);
+      const void* fn = philox_kernel(var, loop, true, waves, false, n_leaves > 0);
       HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
       int n_items = items;
       void* args[] = {&A, &n_items, (void*)&entries, &n_leaves};
