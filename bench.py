@@ -96,11 +96,23 @@ def cpu_model():
     return "unknown"
 
 
+def _latest_profile(suffix):
+    """profiles/r<N>_<suffix> of the latest round that has one ('' when none)."""
+    import glob
+    import re
+    best, path = -1, ""
+    for f in glob.glob(os.path.join(ROOT, "profiles", f"r*_{suffix}")):
+        m = re.match(r"r(\d+)_", os.path.basename(f))
+        if m and int(m.group(1)) > best:
+            best, path = int(m.group(1)), f
+    return path
+
+
 def pmc_traffic(args, kernel_ms):
     """HBM traffic of the render kernel from the committed rocprofv3 PMC summary of the same
     config (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE, bytes per launch), as GB/s over
     this run's live kernel time. None when no summary matches the launched kernel selection."""
-    path = args.traffic_json or os.path.join(ROOT, "profiles", f"r1_pmc_{args.config}.json")
+    path = args.traffic_json or _latest_profile(f"pmc_{args.config}.json")
     default_sel = not any(k.startswith("RTAMD_") for k in os.environ) and not (
         args.nan_cull or args.reference_cull or args.reference_bvh or args.spp or args.tile != 16)
     if not os.path.exists(path) or not (default_sel or args.traffic_json):
@@ -135,7 +147,7 @@ def main():
     ap.add_argument("--no-work", action="store_true", help="skip the counting-build pass")
     ap.add_argument("--traffic-json", default="",
                     help="PMC summary (scripts/pmc_summary.py) of this config's render kernel; default "
-                         "profiles/r1_pmc_<config>.json when the run uses the default kernel selection")
+                         "profiles/r<latest>_pmc_<config>.json when the run uses the default kernel selection")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI, default) or gloo (rehearsal: host-staged gather)")
     args = ap.parse_args()
