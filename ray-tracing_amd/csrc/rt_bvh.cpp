@@ -296,39 +296,20 @@ bool stack_needs(const std::vector<rt_node>& nodes, std::vector<int>& need) {
 // Rebuild the world tree rooted at `root` over its leaves; appends nodes, returns the new root
 // (or `root` unchanged when the tree is not eligible). Eligible: no ConstantMedium anywhere
 // under the root, every leaf boundable, finite boxes.
-int rebuild_world_bvh(std::vector<rt_node>& nodes, int root) {
-  std::vector<int> leaves;
-  std::vector<char> seen(nodes.size(), 0);
-  bool ok = true;
-  std::function<void(int)> walk = [&](int id) {
-    if (!ok) return;
-    const rt_node& n = nodes[id];
-    if (n.type == RT_NODE_BVH) {
-      walk(n.a);
-      walk(n.b);
-      return;
-    }
-    std::function<bool(int)> has_media = [&](int k) -> bool {
-      const rt_node& m = nodes[k];
-      if (m.type == RT_NODE_CONSTANT_MEDIUM) return true;
-      if (m.type == RT_NODE_BVH) return has_media(m.a) || has_media(m.b);
-      if (m.type == RT_NODE_TRANSLATE || m.type == RT_NODE_ROTATE) return has_media(m.a);
-      return false;
-    };
-    if (has_media(id) || n.type == RT_NODE_UNHITTABLE || n.type == RT_NODE_EXT) {
-      ok = false;
-      return;
-    }
-    if (!seen[id]) {  // BVHNode h h (src/Lib.hs:948): test the leaf once — a repeat cannot change the hit
-      seen[id] = 1;
-      leaves.push_back(id);
-    }
-  };
-  if (nodes[root].type != RT_NODE_BVH) return root;
-  walk(root);
-  // Small trees (e.g. the 8-object Cornell box) keep the reference tree: nothing to gain, and its
-  // visiting order was measured faster there.
-  if (!ok || leaves.size() < 16) return root;
+namespace {
+
+bool has_media(const std::vector<rt_node>& nodes, int k) {
+  const rt_node& m = nodes[k];
+  if (m.type == RT_NODE_CONSTANT_MEDIUM) return true;
+  if (m.type == RT_NODE_BVH) return has_media(nodes, m.a) || has_media(nodes, m.b);
+  if (m.type == RT_NODE_TRANSLATE || m.type == RT_NODE_ROTATE) return has_media(nodes, m.a);
+  return false;
+}
+
+// Binned-SAH tree over the given leaves (appended to `nodes`, every node RT_BVH_ORDERED); -1 when a
+// leaf is not boundable or the tree would need a deeper stack than the LDS walk has (a degenerate
+// split sequence, e.g. exponentially spaced centroids, can give such a spine).
+int sah_over_leaves(std::vector<rt_node>& nodes, const std::vector<int>& leaves) {
   Builder b{nodes};
   // RTAMD_SAH_BINS: centroid bins per axis (0 = a full sweep over the sorted centroids)
   if (const char* e = std::getenv("RTAMD_SAH_BINS")) b.bins = std::max(0, std::min(4096, std::atoi(e)));
@@ -337,9 +318,9 @@ int rebuild_world_bvh(std::vector<rt_node>& nodes, int root) {
   b.leaf_ids = leaves;
   for (int a = 0; a < 3; ++a) b.cx[a].resize(n);
   for (int i = 0; i < n; ++i) {
-    if (!flat_box(nodes, leaves[i], &b.boxes[i])) return root;
+    if (!flat_box(nodes, leaves[i], &b.boxes[i])) return -1;
     for (int a = 0; a < 3; ++a) {
-      if (!std::isfinite(b.boxes[i].mn[a]) || !std::isfinite(b.boxes[i].mx[a])) return root;
+      if (!std::isfinite(b.boxes[i].mn[a]) || !std::isfinite(b.boxes[i].mx[a])) return -1;
       b.cx[a][i] = 0.5 * (b.boxes[i].mn[a] + b.boxes[i].mx[a]);
     }
   }
@@ -348,14 +329,105 @@ int rebuild_world_bvh(std::vector<rt_node>& nodes, int root) {
   Box rb;
   const size_t n_before = nodes.size();
   const int new_root = b.build(items, 0, n, rb);
-  // A degenerate split sequence (e.g. exponentially spaced centroids) can give a spine deeper than
-  // the LDS traversal stack; keep the caller's tree then.
   std::vector<int> need;
   if (!stack_needs(nodes, need) || need[new_root] > kMaxStackNeed) {
     nodes.resize(n_before);
-    return root;
+    return -1;
   }
   return new_root;
+}
+
+// The leaves under a BVH subtree: its maximal non-BVH nodes, each once (BVHNode h h, src/Lib.hs:948:
+// a repeated leaf cannot change the closest hit).
+void collect_leaves(const std::vector<rt_node>& nodes, int id, std::vector<int>& out, std::vector<char>& seen) {
+  const rt_node& n = nodes[id];
+  if (n.type == RT_NODE_BVH) {
+    collect_leaves(nodes, n.a, out, seen);
+    collect_leaves(nodes, n.b, out, seen);
+  } else if (!seen[id]) {
+    seen[id] = 1;
+    out.push_back(id);
+  }
+}
+
+}  // namespace
+
+// Rebuild the world tree rooted at `root` over its leaves; appends nodes, returns the new root
+// (or `root` unchanged when the tree is not eligible). Eligible: no ConstantMedium anywhere
+// under the root, no Unhittable leaf, every leaf boundable, finite boxes.
+int rebuild_world_bvh(std::vector<rt_node>& nodes, int root) {
+  if (nodes[root].type != RT_NODE_BVH || has_media(nodes, root)) return root;
+  std::vector<int> leaves;
+  std::vector<char> seen(nodes.size(), 0);
+  collect_leaves(nodes, root, leaves, seen);
+  for (int id : leaves)
+    if (nodes[id].type == RT_NODE_UNHITTABLE || nodes[id].type == RT_NODE_EXT) return root;
+  // Small trees (e.g. the 8-object Cornell box) keep the reference tree: nothing to gain, and its
+  // visiting order was measured faster there.
+  if (leaves.size() < 16) return root;
+  const int r = sah_over_leaves(nodes, leaves);
+  return r < 0 ? root : r;
+}
+
+namespace {
+
+// rebuild_media_skeleton's recursion: the id that replaces node `id` (itself when unchanged).
+int skeleton(std::vector<rt_node>& nodes, int id, int depth) {
+  if (depth > 512) return id;
+  const rt_node n = nodes[id];  // (a copy: `nodes` grows)
+  if (n.type == RT_NODE_BVH) {
+    if (!has_media(nodes, id)) {
+      // a media-free subtree: its leaves, instance frames first rebuilt inside, re-bounded by SAH
+      std::vector<int> leaves;
+      std::vector<char> seen(nodes.size(), 0);
+      collect_leaves(nodes, id, leaves, seen);
+      bool changed = false;
+      for (int& leaf : leaves) {
+        if (nodes[leaf].type == RT_NODE_UNHITTABLE || nodes[leaf].type == RT_NODE_EXT) return id;
+        const int nl = skeleton(nodes, leaf, depth + 1);
+        changed |= nl != leaf;
+        leaf = nl;
+      }
+      if (leaves.size() < 16 && !changed) return id;
+      const int r = sah_over_leaves(nodes, leaves);
+      return r < 0 ? id : r;
+    }
+    const int a = skeleton(nodes, n.a, depth + 1), b = skeleton(nodes, n.b, depth + 1);
+    if (a == n.a && b == n.b) return id;
+    rt_node m = n;  // the skeleton node itself keeps its place, box and left-first order
+    m.a = a;
+    m.b = b;
+    nodes.push_back(m);
+    return (int)nodes.size() - 1;
+  }
+  if (n.type == RT_NODE_TRANSLATE || n.type == RT_NODE_ROTATE) {  // a frame: rebuild inside
+    const int a = skeleton(nodes, n.a, depth + 1);
+    if (a == n.a) return id;
+    rt_node m = n;
+    m.a = a;
+    nodes.push_back(m);
+    return (int)nodes.size() - 1;
+  }
+  return id;  // primitives, chains, media (their boundary is a primitive chain)
+}
+
+}  // namespace
+
+// Worlds the walk must take in the reference's own order (ConstantMedium draws, instance frames):
+// the skeleton of BVH nodes above media stays as it is (left first, the caller's boxes), while every
+// media-free subtree below it — and every tree inside an instance frame — is re-bounded by SAH over
+// the same leaves. A media-free subtree's closest hit (and so the bound the walk carries on with)
+// does not depend on its shape except for exact ties, which the walk detects (rt_trace.h). Returns
+// the new root (== root when nothing changed).
+int rebuild_media_skeleton(std::vector<rt_node>& nodes, int root) {
+  const size_t n0 = nodes.size();
+  const int r = skeleton(nodes, root, 0);
+  std::vector<int> need;
+  if (r != root && (!stack_needs(nodes, need) || need[r] > kMaxStackNeed)) {
+    nodes.resize(n0);
+    return root;
+  }
+  return r;
 }
 
 namespace {
@@ -527,6 +599,34 @@ bool build_wide_bvh(const std::vector<rt_node>& nodes, int root, std::vector<rt_
   return true;
 }
 
+// The world tree the device walks, as rt_upload_scene builds it: worlds with ConstantMedium or
+// instance frames (Translate/Rotate over a BVH) keep their skeleton (rebuild_media_skeleton;
+// RTAMD_SKELETON=0: the caller's tree as is), the others are rebuilt whole (rebuild_world_bvh).
+int rebuild_for_device(std::vector<rt_node>& nodes, int root) {
+  bool media = false, frames = false;
+  std::vector<char> seen(nodes.size(), 0);
+  std::function<void(int)> scan = [&](int id) {
+    if (seen[id]) return;
+    seen[id] = 1;
+    const rt_node& n = nodes[id];
+    if (n.type == RT_NODE_CONSTANT_MEDIUM) media = true;
+    if (n.type == RT_NODE_BVH) {
+      scan(n.a);
+      scan(n.b);
+    } else if (n.type == RT_NODE_TRANSLATE || n.type == RT_NODE_ROTATE) {
+      int k = n.a;
+      while (nodes[k].type == RT_NODE_TRANSLATE || nodes[k].type == RT_NODE_ROTATE) k = nodes[k].a;
+      frames |= nodes[k].type == RT_NODE_BVH || nodes[k].type == RT_NODE_CONSTANT_MEDIUM;
+      scan(n.a);
+    }
+  };
+  scan(root);
+  if (!media && !frames) return rebuild_world_bvh(nodes, root);
+  const char* e = std::getenv("RTAMD_SKELETON");
+  if (e && e[0] == '0') return root;
+  return rebuild_media_skeleton(nodes, root);
+}
+
 }  // namespace rt
 
 extern "C" int rt_rebuild_bvh(const rt_scene_desc* in, rt_node* out_nodes, int capacity, int* out_n, int* out_root) {
@@ -536,7 +636,7 @@ extern "C" int rt_rebuild_bvh(const rt_scene_desc* in, rt_node* out_nodes, int c
     return RT_E_INVALID;
   }
   std::vector<rt_node> nodes(in->nodes, in->nodes + in->n_nodes);
-  const int root = rt::rebuild_world_bvh(nodes, in->world_root);
+  const int root = rt::rebuild_for_device(nodes, in->world_root);
   *out_n = (int)nodes.size();
   *out_root = root;
   if (out_nodes) {

@@ -23,6 +23,8 @@
 #define RT_LIGHT_DEPTH 2  /* max BVH depth of the lights tree (host-validated) */
 #define RT_MAX_FRAMES 4   /* max nesting of instance frames on the replacement loop (host-validated) */
 #define RT_FRAME 0x40000000 /* stack-entry tag: instance frame marker */
+#define RT_SUB 0x20000000   /* node-id tag (walks in the reference's order): inside a re-bounded,
+                               media-free subtree (below an RT_BVH_ORDERED node) */
 #define RT_CHAIN_PRIM 0x100 /* device node type flag: Translate/Rotate chain ending in a primitive */
 #define RT_TYPE_MASK 0xff
 

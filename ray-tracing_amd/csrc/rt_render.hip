@@ -32,6 +32,7 @@
 
 namespace rt {
 int rebuild_world_bvh(std::vector<rt_node>& nodes, int root);
+int rebuild_for_device(std::vector<rt_node>& nodes, int root);
 bool build_wide_bvh(const std::vector<rt_node>& nodes, int root, std::vector<rt_wnode>& out, int* stack_need);
 }
 
@@ -173,8 +174,9 @@ __device__ __forceinline__ bool segment(const RenderArgs& A, const Scene& S, Ray
     return true;
   }
   Hit h;
-  const bool got = traverse<F>(S, S.world, ray, kEps, INFINITY, h, g, stk, !(A.flags & RT_FLAG_REFERENCE_CULL), cnt,
-                               stride);
+  // (worlds walked in the reference's order: the recursive walk takes the caller's tree as is)
+  const bool got = traverse<F>(S, S.ref_walk ? S.world_ref : S.world, ray, kEps, INFINITY, h, g, stk,
+                               !(A.flags & RT_FLAG_REFERENCE_CULL), cnt, stride);
   if constexpr ((F & F_COUNT) != 0) *t_trav = stamp();
   if (!got) {
     contrib = vmul(thr, v3(S.bg[0], S.bg[1], S.bg[2]));
@@ -379,6 +381,9 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
 
   long long w = -1;  // the current chunk's slot in A.partial
   bool done = false, walking = false, ready = false;
+  // (worlds walked in the reference's order) an exact tie was seen in a re-bounded subtree: the
+  // sample is redone from its first draw with every walk on the caller's tree
+  bool force_ref = false;
   int px = 0, row = 0, s = 0, s_end = 0, depth = 0;
   V3 thr = v3(0, 0, 0), sum = v3(0, 0, 0);
   RngPhilox g;
@@ -396,6 +401,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     }
     sum = sum + contrib;
     ++s;
+    if constexpr (kRefMixed<F>) force_ref = false;
     const bool all_nan = (A.flags & RT_FLAG_NAN_CULL) && sum.x != sum.x && sum.y != sum.y && sum.z != sum.z;
     if (s == s_end || all_nan) {
       store_partial(A, w, sum);
@@ -412,8 +418,14 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     // ---- shade finished walks, then set up the next walk for every lane that is not walking
     if (ready && t.tie) {  // exact tie: redo this walk as the reference does
       ready = false;
-      trav_restart_ref(t, S.world_ref, INFINITY);
-      walking = true;
+      if (kRefMixed<F> && S.ref_walk) {
+        // the walk drew for media: redo the whole sample (restarted below from its first draw, so
+        // every draw repeats) on the caller's tree
+        force_ref = true;
+      } else {
+        trav_restart_ref(t, S.world_ref, INFINITY);
+        walking = true;
+      }
     }
     // the next walk's ray: a scattered ray (next segment) or a camera ray (next sample), parked in
     // t.ray (free once the walk's hit is recorded); both kinds of lane start their walk together
@@ -484,7 +496,9 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     }
     if (start) {
       trav_begin<F>(t, plain(t.ray), S.world, kEps, INFINITY);
-      if (S.ref_walk) trav_restart_ref(t, S.world_ref, INFINITY);
+      // worlds with media or frames: the reference's order over the re-bounded skeleton (S.world),
+      // or over the caller's tree itself once this sample saw a tie
+      if (S.ref_walk) trav_restart_ref(t, (kRefMixed<F> && !force_ref) ? S.world : S.world_ref, INFINITY);
       walking = true;
     }
     if (!walking) break;  // this lane is finished; the rest of the wave carries on without it
@@ -661,14 +675,15 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
   Cnt cnt{};
   bool got;
   if (walk == 0) {
-    got = traverse<F>(S, S.world, r, tmin, tmax, h, g, stk, joint != 0, cnt);
+    got = traverse<F>(S, S.ref_walk ? S.world_ref : S.world, r, tmin, tmax, h, g, stk, joint != 0, cnt);
   } else {  // the render loop's resumable walk (binary, or 4-wide under F_WIDE)
     Trav t;
     trav_begin<F>(t, r, S.world, tmin, tmax);
-    if (S.ref_walk) trav_restart_ref(t, S.world_ref, tmax);
+    if (S.ref_walk) trav_restart_ref(t, S.world, tmax);  // (the re-bounded skeleton, mixed walk)
     bool walking = true;
     walk_until<F>(S, t, walking, tmin, stk, RT_BLOCK, joint != 0, 0, 0, cnt, g, side);
     if (t.tie) {
+      if (S.ref_walk) g.init(seed, (uint32_t)i, 0);  // media draws repeat on the caller's tree
       trav_restart_ref(t, S.world_ref, tmax);
       while (trav_step<F>(S, t, tmin, stk, RT_BLOCK, joint != 0, cnt, g, side)) {
       }
@@ -1254,14 +1269,13 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
       rt::set_error("rt_upload_scene: " + v0.err);
       return v0.code;
     }
-    // Only for worlds the replacement loop walks (no instance frames; media are refused by the
-    // rebuild itself): their walks resolve exact ties on the caller's tree (trav_finish).
-    bool frames = false;
-    for (const rt_node& x : v0.nodes)
-      frames |= ((x.type & RT_TYPE_MASK) == RT_NODE_TRANSLATE || (x.type & RT_TYPE_MASK) == RT_NODE_ROTATE) &&
-                !(x.type & RT_CHAIN_PRIM);
-    if (!frames) dd.world_root = rt::rebuild_world_bvh(nodes, din->world_root);
+    // Worlds without media or instance frames: a whole new tree over the same leaves (exact ties are
+    // redone on the caller's tree). Worlds walked in the reference's order (media draws, frames):
+    // the skeleton above the media stays, the media-free subtrees below it (and the trees inside
+    // frames) are re-bounded; RTAMD_SKELETON=0 keeps the caller's tree as is.
+    dd.world_root = rt::rebuild_for_device(nodes, din->world_root);
   }
+  if ((int)nodes.size() >= RT_SUB) return invalid("rt_upload_scene: too many nodes (ids must stay below 2^29)");
   dd.nodes = nodes.data();
   dd.n_nodes = (int)nodes.size();
   const rt_scene_desc* d = &dd;

@@ -535,6 +535,12 @@ struct Side {
   __device__ __forceinline__ int best(int i) const { return p[(14 + RT_MAX_FRAMES + i) * stride]; }
 };
 constexpr int kSubChain = -1, kSubMedium = -2;  // Trav::best_sub of a chain / ConstantMedium hit
+// Kernels that walk media / instance-frame worlds in the reference's order (only the full variant
+// has F_MEDIA and F_FRAMES): there the walk is mixed — the skeleton above media in the reference's
+// semantics, re-bounded media-free subtrees (RT_SUB) with tie detection (rt_bvh.cpp
+// rebuild_media_skeleton).
+template <unsigned F>
+constexpr bool kRefMixed = (F & (F_MEDIA | F_FRAMES)) != 0;
 
 // The same depth-first closest-hit walk as `traverse`, one node per call, with its state kept in
 // registers between calls (stack in LDS), for worlds without ConstantMedium and without instance
@@ -638,12 +644,15 @@ __device__ __forceinline__ void trav_restart_ref(Trav& t, int root, double t_max
 // tie is flagged, and the caller redoes the walk as the reference does it (trav_restart_ref).
 // Exact ties need two surfaces through one point on the ray (e.g. the book-one glass sphere
 // resting on the ground at (0,0,0)); they are rare, so the redo costs nothing measurable.
+// `refsem`: the reference's own semantics for this leaf (a ref walk outside any re-bounded
+// subtree): its bound is `closest` and every accepted hit replaces, as hit BVHNode prefers the
+// right child's hit. Otherwise the bound is closest_up and an exact tie is flagged.
 template <unsigned F>
-__device__ __forceinline__ void trav_take(Trav& t, double x, int id, int sub, Side& side) {
-  if (t.ref || x < t.closest) {  // (ref: every accepted hit replaces, as hit BVHNode prefers the right one)
-    t.best_tmax = t.closest_up;
+__device__ __forceinline__ void trav_take(Trav& t, double x, int id, int sub, Side& side, bool refsem) {
+  if (refsem || x < t.closest) {
+    t.best_tmax = refsem ? t.closest : t.closest_up;
     t.closest = x;
-    t.closest_up = t.ref ? x : nextafter(x, INFINITY);
+    t.closest_up = t.ref ? (kRefMixed<F> ? nextafter(x, INFINITY) : x) : nextafter(x, INFINITY);
     t.best_node = id;
     t.best_sub = sub;
     if constexpr ((F & F_FRAMES) != 0) {
@@ -660,23 +669,24 @@ __device__ __forceinline__ void trav_take(Trav& t, double x, int id, int sub, Si
 // reference's order and under its bound, Lib.hs:1053-1080).
 template <unsigned F, class R>
 __device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, const rt_node* n, int id, double t_min, Cnt& cnt,
-                                          R& g, Side& side) {
+                                          R& g, Side& side, bool refsem) {
   const int type = n->type & RT_TYPE_MASK;
+  const double bound = refsem ? t.closest : t.closest_up;
   if ((F & F_INST) && (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE)) {
     if constexpr ((F & F_COUNT) != 0) ++cnt.other;
     double tt;
-    if (chain_t<F>(S, id, plain(t.ray), t_min, t.closest_up, tt)) trav_take<F>(t, tt, id, kSubChain, side);
-  } else if ((F & F_MEDIA) && type == RT_NODE_CONSTANT_MEDIUM) {
+    if (chain_t<F>(S, id, plain(t.ray), t_min, bound, tt)) trav_take<F>(t, tt, id, kSubChain, side, refsem);
+  } else if ((F & F_MEDIA) && type == RT_NODE_CONSTANT_MEDIUM) {  // (always on the skeleton: refsem)
     if constexpr ((F & F_COUNT) != 0) ++cnt.other;
     Hit h;
-    if (medium_hit<F>(S, n, plain(t.ray), t_min, t.closest, g, h)) trav_take<F>(t, h.t, id, kSubMedium, side);
+    if (medium_hit<F>(S, n, plain(t.ray), t_min, t.closest, g, h)) trav_take<F>(t, h.t, id, kSubMedium, side, true);
   } else {
     if constexpr ((F & F_COUNT) != 0) ++cnt.prim;
     double tt;
     int sub;
-    if (prim_t<F>(S, n, t.ray, t_min, t.closest_up, tt, sub)) {
+    if (prim_t<F>(S, n, t.ray, t_min, bound, tt, sub)) {
       if constexpr ((F & F_COUNT) != 0) ++cnt.phit;
-      trav_take<F>(t, tt, id, sub, side);
+      trav_take<F>(t, tt, id, sub, side, refsem);
     }
   }
 }
@@ -770,34 +780,40 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
       if (wide_node(S, t, stk, stride)) return true;
     } else {
       const rt_node* n = &S.leaves[~t.node];
-      trav_leaf<F>(S, t, n, n->c, t_min, cnt, g, side);
+      trav_leaf<F>(S, t, n, n->c, t_min, cnt, g, side, false);
     }
     if (t.sp == 0) return false;
     t.node = stk[(--t.sp) * stride];
     return true;
   }
-  const rt_node* n = &S.nodes[t.node];
+  // (mixed walks: the RT_SUB tag of the node id says whether it lies below an RT_BVH_ORDERED node)
+  const int id = kRefMixed<F> ? (t.node & ~RT_SUB) : t.node;
+  const int tag = kRefMixed<F> ? (t.node & RT_SUB) : 0;
+  const bool refsem = t.ref && !tag;
+  const rt_node* n = &S.nodes[id];
   const int tf = n->type;
   const int type = tf & RT_TYPE_MASK;
   if (type == RT_NODE_BVH) {
     if constexpr ((F & F_COUNT) != 0) ++cnt.box;
-    if (box_hit(n->f, t.ray, t_min, t.closest_up, joint)) {
+    if (box_hit(n->f, t.ray, t_min, refsem ? t.closest : t.closest_up, joint)) {
       const int c = n->c;
-      const bool flip = (c & RT_BVH_ORDERED) && comp(t.ray.d, c & 3) < 0;
-      stk[(t.sp++) * stride] = flip ? n->a : n->b;
-      t.node = flip ? n->b : n->a;
+      const bool ord = (c & RT_BVH_ORDERED) != 0;
+      const bool flip = ord && comp(t.ray.d, c & 3) < 0;
+      const int ctag = (kRefMixed<F> && ord) ? RT_SUB : tag;
+      stk[(t.sp++) * stride] = (flip ? n->a : n->b) | ctag;
+      t.node = (flip ? n->b : n->a) | ctag;
       return true;
     }
   } else if ((F & F_FRAMES) && (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE) && !(tf & RT_CHAIN_PRIM)) {
     if constexpr ((F & F_COUNT) != 0) ++cnt.other;
     if (t.level == 0) side.put_ray(plain(t.ray));
-    side.frame(t.level++) = t.node;
-    stk[(t.sp++) * stride] = RT_FRAME | t.node;
+    side.frame(t.level++) = id;
+    stk[(t.sp++) * stride] = RT_FRAME | id;
     t.ray = prep(enter_instance(n, plain(t.ray)));
-    t.node = n->a;
+    t.node = n->a | tag;
     return true;
   } else {
-    trav_leaf<F>(S, t, n, t.node, t_min, cnt, g, side);
+    trav_leaf<F>(S, t, n, id, t_min, cnt, g, side, refsem);
   }
   for (;;) {
     if (t.sp == 0) return false;
@@ -842,7 +858,7 @@ __device__ __forceinline__ void wide_leaf(const Scene& S, Trav& t, double t_min,
                                           Side& side) {
   if (t.pend >= 0) {
     const rt_node* n = &S.leaves[t.pend];  // (pend holds the leaf table slot)
-    trav_leaf<F>(S, t, n, n->c, t_min, cnt, g, side);
+    trav_leaf<F>(S, t, n, n->c, t_min, cnt, g, side, false);
     t.pend = -1;
   }
   trav_postpone(t, stk, stride);

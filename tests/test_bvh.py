@@ -64,10 +64,95 @@ def test_rebuilt_tree_is_a_proper_bvh():
     assert np.all((new["c"] & rtamd.RT_BVH_ORDERED) != 0) and np.all((new["c"] & 3) <= 2)
 
 
-@pytest.mark.parametrize("name", ["cornell_smoke", "next_week_final", "cornell", "three_spheres"])
-def test_media_and_small_trees_are_not_rebuilt(name):
+@pytest.mark.parametrize("name", ["cornell_smoke", "cornell", "three_spheres"])
+def test_small_trees_are_not_rebuilt(name):
+    """Worlds whose media-free subtrees all hold < 16 leaves keep the caller's tree."""
     scene, _ = rtamd.make_scene(name, rtamd.randGen(1024))
     assert rtamd.rebuilt_scene(scene).desc.world_root == scene.desc.world_root
+
+
+def _earth():
+    import os
+    return np.load(os.path.join(os.path.dirname(__file__), "golden", "earthmap_rgb8.npz"))["rgb"]
+
+
+def test_media_world_keeps_its_skeleton():
+    """next_week_final (two ConstantMedium, a Translate/Rotate frame over 1000 spheres): the BVH
+    nodes above the media keep their boxes, children order and left-first semantics (no
+    RT_BVH_ORDERED); everything below an ORDERED node is media-free; the media nodes themselves and
+    every leaf are the caller's records (same ids); the frame's inner tree is re-bounded too."""
+    scene, _ = rtamd.make_scene("next_week_final", rtamd.randGen(1024), earth=_earth())
+    rb = rtamd.rebuilt_scene(scene)
+    old, new = scene.nodes, rb.nodes
+    n0 = scene.desc.n_nodes
+    assert rb.desc.world_root != scene.desc.world_root and rb.desc.n_nodes > n0
+    assert np.array_equal(new[:n0], old)  # the caller's records are untouched (appended only)
+
+    def has_media(nodes, i):
+        t = int(nodes[i]["type"])
+        if t == rtamd.RT_NODE_CONSTANT_MEDIUM:
+            return True
+        if t == rtamd.RT_NODE_BVH:
+            return has_media(nodes, int(nodes[i]["a"])) or has_media(nodes, int(nodes[i]["b"]))
+        if t in (rtamd.RT_NODE_TRANSLATE, rtamd.RT_NODE_ROTATE):
+            return has_media(nodes, int(nodes[i]["a"]))
+        return False
+
+    def media_ids(nodes, i, out):
+        nd = nodes[i]
+        t = int(nd["type"])
+        if t == rtamd.RT_NODE_CONSTANT_MEDIUM:
+            out.append(i)
+        elif t == rtamd.RT_NODE_BVH:
+            media_ids(nodes, int(nd["a"]), out)
+            media_ids(nodes, int(nd["b"]), out)
+        elif t in (rtamd.RT_NODE_TRANSLATE, rtamd.RT_NODE_ROTATE):
+            media_ids(nodes, int(nd["a"]), out)
+        return out
+
+    ordered_frames = 0
+
+    def check(i, below_ordered):
+        nonlocal ordered_frames
+        nd = new[i]
+        t = int(nd["type"])
+        if t == rtamd.RT_NODE_BVH:
+            ordered = (int(nd["c"]) & rtamd.RT_BVH_ORDERED) != 0
+            if has_media(new, i):
+                assert not ordered and not below_ordered  # skeleton
+            if ordered and i >= n0:
+                assert not has_media(new, i)
+            check(int(nd["a"]), below_ordered or ordered)
+            check(int(nd["b"]), below_ordered or ordered)
+        elif t in (rtamd.RT_NODE_TRANSLATE, rtamd.RT_NODE_ROTATE):
+            inner = int(new[int(nd["a"])]["c"]) if int(new[int(nd["a"])]["type"]) == rtamd.RT_NODE_BVH else 0
+            ordered_frames += (inner & rtamd.RT_BVH_ORDERED) != 0
+            check(int(nd["a"]), below_ordered)
+    check(rb.desc.world_root, False)
+    assert ordered_frames >= 1
+    assert media_ids(new, rb.desc.world_root, []) == media_ids(old, scene.desc.world_root, [])
+
+
+@pytest.mark.parametrize("name", ["next_week_final", "cornell_smoke"])
+def test_skeleton_gives_the_references_closest_hits_and_draws(name):
+    """The oracle (the reference's own hit recursion, media draws included) over the device's tree
+    and over the caller's tree: every closest hit identical, including medium hits, whose draw
+    depends on the bound the walk carries when it reaches the medium."""
+    scene, _ = rtamd.make_scene(name, rtamd.randGen(1024), earth=_earth() if name == "next_week_final" else None)
+    rb = rtamd.rebuilt_scene(scene)
+    rng = np.random.default_rng(11)
+    n = 20000
+    if name == "next_week_final":
+        o = np.array([478.0, 278.0, -600.0]) + rng.normal(0, 30, (n, 3))
+        d = np.array([-200.0, 0.0, 600.0]) - np.array([478.0, 278.0, -600.0]) + rng.normal(0, 250, (n, 3))
+    else:
+        o = rng.uniform(20, 530, (n, 3))
+        d = rng.normal(0, 1, (n, 3))
+    rays = np.concatenate([o, d, rng.uniform(0, 1, (n, 1))], axis=1)
+    a = pyoracle.closest_hits(scene, rays, 1e-4, np.inf, seed=5)
+    b = pyoracle.closest_hits(rb, rays, 1e-4, np.inf, seed=5)
+    assert a[:, 0].sum() > n // 4
+    assert np.array_equal(a, b)
 
 
 @pytest.mark.parametrize("name,param", [("random_book_one", 0), ("stress_spheres", 3000), ("cornell", 0),
