@@ -279,10 +279,10 @@ def main():
             slots = work.pop("lane_slots")
             leaf_hits = work.pop("leaf_hits")
             if slots["outer_iterations"]:  # lane utilisation of the replacement loop's phases
-                out["lane_utilisation"] = {
-                    "wide_steps": round(work["wide_nodes"] / max(1, slots["wide_steps"]), 4),
-                    "leaf_steps": round(work["prim_tests"] / max(1, slots["leaf_steps"]), 4),
-                    "shade": round(work["segments"] / max(1, slots["outer_iterations"]), 4)}
+                out["lane_utilisation"] = {"shade": round(work["segments"] / slots["outer_iterations"], 4)}
+                if slots["wide_steps"] and slots["leaf_steps"]:  # (the 4-wide walk's two kinds of step)
+                    out["lane_utilisation"]["wide_steps"] = round(work["wide_nodes"] / slots["wide_steps"], 4)
+                    out["lane_utilisation"]["leaf_steps"] = round(work["prim_tests"] / slots["leaf_steps"], 4)
             per = {k: work[k] / n for k in work}
             bytes_per_sample = sum(BYTES[k] * per[k] for k in BYTES) + 3.0 / cfg["spp"]
             flops_per_sample = sum(FLOPS[k] * per[k] for k in FLOPS)
