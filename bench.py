@@ -277,7 +277,7 @@ def main():
             n = max(1, work["samples"])
             out["phase_split"] = {k: round(v, 4) for k, v in work.pop("phase_split").items()}
             slots = work.pop("lane_slots")
-            leaf_hits = work.pop("leaf_hits")
+            leaf_hits, tie_redos = work.pop("leaf_hits"), work.pop("tie_redos")
             if slots["outer_iterations"]:  # lane utilisation of the replacement loop's phases
                 out["lane_utilisation"] = {"shade": round(work["segments"] / slots["outer_iterations"], 4)}
                 if slots["wide_steps"] and slots["leaf_steps"]:  # (the 4-wide walk's two kinds of step)
@@ -307,6 +307,7 @@ def main():
                            "frac": round(fl32 / FP32_PEAK_TFLOPS, 5), "flops_per_sample": round(f32, 1)}
             out["work_per_sample"] = {k: round(v, 3) for k, v in per.items() if k != "samples"}
             out["work_per_sample"]["leaf_hits"] = round(leaf_hits / n, 3)
+            out["work_per_sample"]["tie_redos"] = round(tie_redos / n, 5)
             if counters:
                 out["work_per_sample_reference_cull"] = {k: round(v / max(1, counters["samples"]), 3)
                                                          for k, v in counters.items() if k != "samples"}

@@ -363,7 +363,8 @@ int rt_assemble_linear_async(rt_ctx* ctx, const rt_render_params* p, const doubl
  * for this shard; out_work[8..10] = wave time (s_memtime ticks, summed over waves) spent acquiring work and
  * starting samples / traversing / shading; out_work[11..13] (ray-replacement loop only) = live-lane
  * slots of 4-wide node steps, of leaf steps and of outer iterations (lane utilisation = work / slots);
- * out_work[14] = leaf tests that found a hit (replacement loop); the rest 0.
+ * out_work[14] = leaf tests that found a hit, out_work[15] = walks redone for an exact tie (worlds
+ * with media or frames: samples redone) (replacement loop).
  */
 int rt_render_work(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* p, uint64_t out_work[16]);
 

@@ -222,6 +222,18 @@ struct RngPhilox {
       n += 2;
     }
   }
+  // Words of this stream consumed so far (word i is word i % 2 of block i / 2), and the state after
+  // exactly `c` of them: a walk that has to be redone can repeat its draws.
+  __device__ __forceinline__ uint32_t consumed() const { return 2u * pair - n; }
+  __device__ __forceinline__ void rewind(uint32_t c) {
+    pair = c >> 1;
+    n = 0;
+    if (c & 1u) {
+      uint64_t x;
+      block(x, w0);
+      n = 1;
+    }
+  }
   __device__ __forceinline__ double draw() {
     if (n == 0) block(w0, w1), n = 2;  // not reserved: compute here
     const uint64_t w = w0;

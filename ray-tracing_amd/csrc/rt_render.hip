@@ -381,9 +381,9 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
 
   long long w = -1;  // the current chunk's slot in A.partial
   bool done = false, walking = false, ready = false;
-  // (worlds walked in the reference's order) an exact tie was seen in a re-bounded subtree: the
-  // sample is redone from its first draw with every walk on the caller's tree
-  bool force_ref = false;
+  // (worlds walked in the reference's order) the stream position at the start of the walk: a walk
+  // redone for an exact tie repeats its media draws
+  uint32_t walk_mark = 0;
   int px = 0, row = 0, s = 0, s_end = 0, depth = 0;
   V3 thr = v3(0, 0, 0), sum = v3(0, 0, 0);
   RngPhilox g;
@@ -401,7 +401,6 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     }
     sum = sum + contrib;
     ++s;
-    if constexpr (kRefMixed<F>) force_ref = false;
     const bool all_nan = (A.flags & RT_FLAG_NAN_CULL) && sum.x != sum.x && sum.y != sum.y && sum.z != sum.z;
     if (s == s_end || all_nan) {
       store_partial(A, w, sum);
@@ -418,14 +417,10 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     // ---- shade finished walks, then set up the next walk for every lane that is not walking
     if (ready && t.tie) {  // exact tie: redo this walk as the reference does
       ready = false;
-      if (kRefMixed<F> && S.ref_walk) {
-        // the walk drew for media: redo the whole sample (restarted below from its first draw, so
-        // every draw repeats) on the caller's tree
-        force_ref = true;
-      } else {
-        trav_restart_ref(t, S.world_ref, INFINITY);
-        walking = true;
-      }
+      if constexpr ((F & F_COUNT) != 0) ++cnt.ties;
+      if constexpr (kRefMixed<F>) g.rewind(walk_mark);  // (the walk's media draws repeat)
+      trav_restart_ref(t, S.world_ref, INFINITY);
+      walking = true;
     }
     // the next walk's ray: a scattered ray (next segment) or a camera ray (next sample), parked in
     // t.ray (free once the walk's hit is recorded); both kinds of lane start their walk together
@@ -496,9 +491,9 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     }
     if (start) {
       trav_begin<F>(t, plain(t.ray), S.world, kEps, INFINITY);
-      // worlds with media or frames: the reference's order over the re-bounded skeleton (S.world),
-      // or over the caller's tree itself once this sample saw a tie
-      if (S.ref_walk) trav_restart_ref(t, (kRefMixed<F> && !force_ref) ? S.world : S.world_ref, INFINITY);
+      // worlds with media or frames: the reference's order over the re-bounded skeleton
+      if (S.ref_walk) trav_restart_ref(t, S.world, INFINITY);
+      if constexpr (kRefMixed<F>) walk_mark = g.consumed();
       walking = true;
     }
     if (!walking) break;  // this lane is finished; the rest of the wave carries on without it
@@ -529,6 +524,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     wave_add(&A.work[12], cnt.lslot);
     wave_add(&A.work[13], cnt.oslot);
     wave_add(&A.work[14], cnt.phit);
+    wave_add(&A.work[15], cnt.ties);
     if ((threadIdx.x & 63) == 0) {
       atomicAdd(&A.work[8], ph_setup);
       atomicAdd(&A.work[9], ph_trav);
@@ -683,7 +679,7 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
     bool walking = true;
     walk_until<F>(S, t, walking, tmin, stk, RT_BLOCK, joint != 0, 0, 0, cnt, g, side);
     if (t.tie) {
-      if (S.ref_walk) g.init(seed, (uint32_t)i, 0);  // media draws repeat on the caller's tree
+      if (S.ref_walk) g.rewind(0);  // media draws repeat on the caller's tree
       trav_restart_ref(t, S.world_ref, tmax);
       while (trav_step<F>(S, t, tmin, stk, RT_BLOCK, joint != 0, cnt, g, side)) {
       }

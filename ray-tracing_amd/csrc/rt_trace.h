@@ -24,6 +24,7 @@ struct Cnt {
   unsigned box, prim, other, light, wide;
   unsigned islot, lslot, oslot;  // lane slots (live lanes) of wide-node steps, leaf steps, outer iterations
   unsigned phit;                 // leaf tests that found a hit
+  unsigned ties;                 // walks redone for an exact tie
 };
 
 // ------------------------------------------------------------------ textures (Lib.hs:441-513)

@@ -517,6 +517,7 @@ class Context:
         # replacement loop only: live-lane slots of 4-wide node steps, leaf steps and outer iterations
         out["lane_slots"] = {"wide_steps": int(w[11]), "leaf_steps": int(w[12]), "outer_iterations": int(w[13])}
         out["leaf_hits"] = int(w[14])  # replacement loop only: leaf tests that found a hit
+        out["tie_redos"] = int(w[15])  # replacement loop only: walks (or samples) redone for an exact tie
         return out
 
     def last_kernel_ms(self) -> float:
