@@ -84,6 +84,8 @@ struct RenderArgs {
   unsigned long long* counter;
   unsigned long long* work;  // counting build: [segments, box, prim, other, light, blocks, samples]
   int trav_stop;             // replacement loop: keep stepping while > trav_stop/64 of live lanes walk
+  int batch;                 // replacement loop: most work-items a wave claims per atomic
+  float batch_per_item;      // ...tapering to rem * batch_per_item as `rem` items remain (>= need)
   int leaf_stop;             // 4-wide walk: leaf step once <= leaf_stop/64 of live lanes seek a leaf
   uint8_t* out_rgb;  // tier B: slab; tier A: image
   double* out_lin;
@@ -374,7 +376,8 @@ __global__ void __launch_bounds__(WAVES * 256, WAVES) render_philox_lds(RenderAr
 // node at a time until at most trav_stop/64 of the live lanes are still walking. Lanes never
 // wait for the slowest walk of their wave, and shading runs for many lanes at once.
 template <unsigned F>
-__device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S, int* stk, int stride, int* side_p) {
+__device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S, int* stk, int stride, int* side_p,
+                                             volatile uint32_t* wq) {
   const int lane = threadIdx.x & 63;
   const unsigned long long lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const bool joint = !(A.flags & RT_FLAG_REFERENCE_CULL);
@@ -384,6 +387,13 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
   // (worlds walked in the reference's order) the stream position at the start of the walk: a walk
   // redone for an exact tie repeats its media draws
   uint32_t walk_mark = 0;
+  // wq[0..1]: the wave's claimed, not yet handed out work-items [next, end), in LDS (lanes that
+  // are walking skip the acquisition code, so a per-lane copy would go stale); indices are < 2^32
+  // (launch_philox checks)
+  if (lane == 0) {
+    wq[0] = 0u;
+    wq[1] = 0u;
+  }
   int px = 0, row = 0, s = 0, s_end = 0, depth = 0;
   V3 thr = v3(0, 0, 0), sum = v3(0, 0, 0);
   RngPhilox g;
@@ -447,17 +457,39 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     unsigned long long s0b = 0;
     if constexpr ((F & F_COUNT) != 0) s0b = stamp();
     while (!walking && !start) {
-      // acquire pixels for idle lanes: one atomic per round for all of them
+      // acquire work-items for idle lanes: from the wave's claimed range first; when it runs short,
+      // one atomic claims a batch of A.batch more (exactly the lanes' need once the counter is near
+      // the end, so that no wave hoards the frame's last items)
       for (;;) {
         const bool need = (w < 0) && !done;
         const unsigned long long mask = __ballot(need);
         if (!mask) break;
-        const int leader = __ffsll((long long)mask) - 1;
-        unsigned long long base = 0;
-        if (lane == leader) base = atomicAdd(A.counter, (unsigned long long)__popcll(mask));
-        base = __shfl(base, leader);
+        const uint32_t n_need = (uint32_t)__popcll(mask);
+        const uint32_t q_next = wq[0], q_end = wq[1];
+        const uint32_t avail = q_end - q_next;
+        uint32_t base2 = q_next, end2 = q_end;  // items past `avail` come from a new claim
+        if (avail < n_need) {
+          const int leader = __ffsll((long long)mask) - 1;
+          unsigned long long claim = 0;
+          if (lane == leader) {
+            // batch: A.batch items, fewer as the frame runs out (the wave's last claim end tells it
+            // roughly how many remain), so that no wave hoards the tail; never less than the need
+            const uint32_t want = n_need - avail;
+            const long long rem = A.work_total - (long long)q_end;
+            const uint32_t b = rem <= 0 ? 0u : (uint32_t)fminf((float)A.batch, (float)rem * A.batch_per_item);
+            const uint32_t got = want < b ? b : want;
+            const unsigned long long c0 = atomicAdd(A.counter, (unsigned long long)got);
+            // (claims past 2^32 only happen once every item is handed out: clamp, the lanes see
+            // `done`); the claim and its size travel together in one broadcast
+            claim = (c0 < 0xffff0000ull ? c0 : 0xffff0000ull) | ((unsigned long long)got << 32);
+          }
+          const unsigned long long c1 = __shfl(claim, leader);
+          base2 = (uint32_t)c1;
+          end2 = base2 + (uint32_t)(c1 >> 32);
+        }
+        const uint32_t rank = (uint32_t)__popcll(mask & lanes_below);
         if (need) {
-          const long long wi = (long long)(base + __popcll(mask & lanes_below));
+          const long long wi = (long long)(rank < avail ? q_next + rank : base2 + (rank - avail));
           if (wi >= A.work_total) {
             done = true;
           } else if (work_item(A, (uint32_t)wi, px, row, s, s_end, w)) {
@@ -465,6 +497,11 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
           } else {
             w = -1;
           }
+        }
+        const int leader = __ffsll((long long)mask) - 1;
+        if (lane == leader) {
+          wq[0] = avail < n_need ? base2 + (n_need - avail) : q_next + n_need;
+          wq[1] = end2;
         }
       }
       if (w < 0) break;  // no work left for this lane
@@ -542,8 +579,10 @@ constexpr int lane_ints() {
 template <unsigned F, int WAVES>
 __global__ void __launch_bounds__(RT_BLOCK, WAVES) render_philox2(RenderArgs A) {
   __shared__ int stk_mem[lane_ints<F>() * RT_BLOCK];
+  __shared__ uint32_t wave_q[RT_BLOCK / 64][2];
   constexpr int stack = (F & F_WIDE) ? RT_WSTACK : RT_STACK;
-  philox_loop2<F>(A, A.S, &stk_mem[threadIdx.x], RT_BLOCK, &stk_mem[stack * RT_BLOCK + threadIdx.x]);
+  philox_loop2<F>(A, A.S, &stk_mem[threadIdx.x], RT_BLOCK, &stk_mem[stack * RT_BLOCK + threadIdx.x],
+                  wave_q[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)]);
 }
 
 // LDS-staged replacement loop: the traversal's node array (the wide records for F_WIDE, else the
@@ -556,6 +595,7 @@ template <unsigned F, int WAVES, bool LEAF_LDS = false>
 __global__ void __launch_bounds__(WAVES * 256, WAVES)
     render_philox2_lds(RenderArgs A, int n_nodes, int stack_entries, int n_leaves) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  __shared__ uint32_t wave_q[WAVES * 4][2];  // (static: kStaticLds bytes ahead of the dynamic LDS)
   constexpr int rec = (F & F_WIDE) ? (int)sizeof(rt_wnode) : (int)sizeof(rt_node);
   {
     const uint4* src = (F & F_WIDE) ? reinterpret_cast<const uint4*>(A.S.wnodes)
@@ -578,7 +618,8 @@ __global__ void __launch_bounds__(WAVES * 256, WAVES)
   int* stk = reinterpret_cast<int*>(lds + (size_t)n_nodes * rec + (size_t)n_leaves * sizeof(rt_node)) + threadIdx.x;
   // (the host sizes the dynamic LDS for stack_entries stack ints + kSideInts Side ints per lane
   // when F has F_FRAMES)
-  philox_loop2<F>(A, S, stk, WAVES * 256, stk + stack_entries * WAVES * 256);
+  philox_loop2<F>(A, S, stk, WAVES * 256, stk + stack_entries * WAVES * 256,
+                  wave_q[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)]);
 }
 
 // Tier B: a slab pixel's chunk sums added in chunk order, then averaged and stored (rt.h).
@@ -955,6 +996,10 @@ void geometry(const rt_render_params* p, int& tile, int& tiles_x, long long& til
   slab_pixels = per_shard * tile * tile;
 }
 
+// Dynamic LDS a CU's workgroup may take: 160 KiB less the replacement loop's static per-wave work
+// queues (16 waves x 8 B).
+constexpr size_t kLdsBudget = 160 * 1024 - 16 * 8;
+
 // Kernel variants: spheres-only (configs 1, 2, 5), Cornell-like (rects, instances, lights), full.
 constexpr unsigned kVarSpheres = 0u;
 constexpr unsigned kVarCornell = F_RECT | F_INST | F_LIGHTS;
@@ -1085,6 +1130,9 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   A.shard_count = shards;
   A.slab = slab;
   A.chunk = rt_sample_chunk((int64_t)p->width * p->height, p->spp);
+  // RTAMD_CHUNK: another chunk size, for timing experiments only (it changes the summation order,
+  // so the image no longer follows rt.h's tier-B definition)
+  if (const char* ce = std::getenv("RTAMD_CHUNK")) A.chunk = std::max(1, std::min(p->spp, std::atoi(ce)));
   A.chunks = (p->spp + A.chunk - 1) / A.chunk;
   A.work_total = slab * A.chunks;
   if (A.work_total >= (1ll << 32)) return invalid("image too large: more than 2^32 work-items per shard");
@@ -1117,6 +1165,16 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   // refill when at most trav_stop/64 of a wave's live lanes still walk (measured: C2 flat at 2-8,
   // -4 % at 16; the 100k-sphere C5 tree, walks ~3x longer, best at 16)
   // (the full variant's walks over the caller's tree: 16, C4 1496 vs 1567 ms at 200 spp)
+  // Work-items a wave claims per atomic: one claim per batch instead of one per acquisition round
+  // (RTAMD_BATCH; 1 = the lanes' exact need every time). The batch tapers as the frame runs out: a
+  // wave claims at most rem / (16 * waves) items when about `rem` remain, so the waves' unstarted
+  // claims together never exceed 1/16 of what is left.
+  {
+    const char* be = std::getenv("RTAMD_BATCH");
+    A.batch = be ? std::max(1, std::min(4096, std::atoi(be))) : 128;
+    const double waves = (double)c->cu_count * 4 * 4;  // at most 4 waves per SIMD
+    A.batch_per_item = (float)(1.0 / (16.0 * waves));
+  }
   A.trav_stop = stop_env ? std::max(0, std::min(63, std::atoi(stop_env)))
                          : (c->n_nodes > 20000 || variant_for(c->features) == F_ALL ? 16 : 8);
   const char* leaf_env = std::getenv("RTAMD_LEAF_STOP");
@@ -1155,17 +1213,17 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
     // when it fits as well
     auto lds_bytes = [&](int w, int& n_leaves) {
       size_t b = (size_t)items * rec + (size_t)(entries + side_ints) * (w * 256) * sizeof(int);
-      n_leaves = leaf_lds && b + (size_t)c->n_leaves * sizeof(rt_node) <= 160 * 1024 ? c->n_leaves : 0;
+      n_leaves = leaf_lds && b + (size_t)c->n_leaves * sizeof(rt_node) <= kLdsBudget ? c->n_leaves : 0;
       return b + (size_t)n_leaves * sizeof(rt_node);
     };
     int n_leaves = 0;
     // (and only when there is work for the 4th wave: C1's 20 000 items fill less than 3 waves)
-    if (var == kVarSpheres && !std::getenv("RTAMD_WAVES") && lds_bytes(4, n_leaves) <= 160 * 1024 &&
+    if (var == kVarSpheres && !std::getenv("RTAMD_WAVES") && lds_bytes(4, n_leaves) <= kLdsBudget &&
         (!leaf_lds || n_leaves > 0) && A.work_total >= (long long)c->cu_count * 1024)
       waves = 4;
     const int block = waves * 256;
     const size_t bytes = lds_bytes(waves, n_leaves);
-    if (bytes <= 160 * 1024) {
+    if (bytes <= kLdsBudget) {
       const void* fn = philox_kernel(var, loop, true, waves, false, n_leaves > 0);
       HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
       int n_items = items;
