@@ -180,13 +180,17 @@ typedef struct rt_camera {
  */
 #define RT_RNG_EXACT 0
 #define RT_RNG_PHILOX 1
-#define RT_CHUNK_SAMPLES 32  /* samples per chunk (C2 on MI355X: 186.4 ms at 32, 187.6 at 64, 205 at 16) */
-#define RT_CHUNK_ITEMS (1 << 20) /* ...fewer when the frame would have fewer work-items than this */
-/* CH = min(spp, 32, max(1, ceil(pixels * spp / 2^20))): 32-sample chunks, except that small frames
-   (e.g. config 1: 200x100x10) use shorter ones so that they still fill the device. */
+#define RT_CHUNK_SAMPLES 8      /* samples per chunk, at least (short chunks: a short tail per shard) */
+#define RT_CHUNK_MAX 64          /* ...but at most this many chunks per pixel (bounds the chunk sums) */
+#define RT_CHUNK_ITEMS (1 << 20) /* ...fewer samples when the frame would have fewer work-items */
+/* CH = min(spp, max(8, ceil(spp / 64)), max(1, ceil(pixels * spp / 2^20))): 8-sample chunks
+   (C2), longer ones for high spp (C3/C4 1000 spp: 16, C5 2000 spp: 32) so that a pixel has at most
+   64, and shorter ones for small frames (config 1: 200x100x10 -> 1) so that they fill the device. */
 static inline int rt_sample_chunk(int64_t pixels, int spp) {
   const int64_t fill = (pixels * (int64_t)spp + RT_CHUNK_ITEMS - 1) / RT_CHUNK_ITEMS;
-  int ch = spp < RT_CHUNK_SAMPLES ? spp : RT_CHUNK_SAMPLES;
+  int ch = (spp + RT_CHUNK_MAX - 1) / RT_CHUNK_MAX;
+  if (ch < RT_CHUNK_SAMPLES) ch = RT_CHUNK_SAMPLES;
+  if (ch > spp) ch = spp;
   if (fill < ch) ch = (int)fill;
   return ch > 0 ? ch : 1;
 }
