@@ -772,6 +772,7 @@ struct rt_ctx {
   // Recorded after every tier-B launch: the next launch (on any stream) waits on it before it
   // resets the shared work counter and reuses the chunk-sum buffer.
   hipEvent_t ev_done = nullptr;
+  hipStream_t last_stream = nullptr;  // the stream of the last tier-B launch (ev_done's)
   // device scene
   rt_node* d_nodes = nullptr;
   DMat* d_mats = nullptr;
@@ -1146,8 +1147,9 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   A.out_rgb = d_rgb;
   A.out_lin = d_lin;
   // The work counter and the chunk-sum buffer are the ctx's: order this launch after the previous
-  // one, whichever stream that was on.
-  HIPCHK(hipStreamWaitEvent(st, c->ev_done, 0));
+  // one, whichever stream that was on (on the same stream, stream order already does).
+  if (st != c->last_stream) HIPCHK(hipStreamWaitEvent(st, c->ev_done, 0));
+  c->last_stream = st;
   {  // chunk sums: [chunk][slab pixel][3] doubles, kept on the ctx and grown on demand
     const size_t need = (size_t)A.chunks * (size_t)slab * 3 * sizeof(double);
     if (need > c->partial_bytes) {
