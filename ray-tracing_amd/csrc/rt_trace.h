@@ -536,6 +536,9 @@ struct Side {
   __device__ __forceinline__ int best(int i) const { return p[(14 + RT_MAX_FRAMES + i) * stride]; }
 };
 constexpr int kSubChain = -1, kSubMedium = -2;  // Trav::best_sub of a chain / ConstantMedium hit
+// Trav::best_node of a leaf found by the 4-wide walk: its leaf-table slot | kSlotTag, so that the
+// record is built from the (LDS-staged) leaf table rather than the flat node array in HBM
+constexpr int kSlotTag = 0x40000000;
 // Kernels that walk media / instance-frame worlds in the reference's order (only the full variant
 // has F_MEDIA and F_FRAMES): there the walk is mixed — the skeleton above media in the reference's
 // semantics, re-bounded media-free subtrees (RT_SUB) with tie detection (rt_bvh.cpp
@@ -676,7 +679,8 @@ __device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, const rt_node
   if ((F & F_INST) && (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE)) {
     if constexpr ((F & F_COUNT) != 0) ++cnt.other;
     double tt;
-    if (chain_t<F>(S, id, plain(t.ray), t_min, bound, tt)) trav_take<F>(t, tt, id, kSubChain, side, refsem);
+    const int flat = (id & kSlotTag) ? n->c : id;  // (the chain is walked in the flat node array)
+    if (chain_t<F>(S, flat, plain(t.ray), t_min, bound, tt)) trav_take<F>(t, tt, id, kSubChain, side, refsem);
   } else if ((F & F_MEDIA) && type == RT_NODE_CONSTANT_MEDIUM) {  // (always on the skeleton: refsem)
     if constexpr ((F & F_COUNT) != 0) ++cnt.other;
     Hit h;
@@ -781,7 +785,7 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
       if (wide_node(S, t, stk, stride)) return true;
     } else {
       const rt_node* n = &S.leaves[~t.node];
-      trav_leaf<F>(S, t, n, n->c, t_min, cnt, g, side, false);
+      trav_leaf<F>(S, t, n, ~t.node | kSlotTag, t_min, cnt, g, side, false);
     }
     if (t.sp == 0) return false;
     t.node = stk[(--t.sp) * stride];
@@ -859,7 +863,7 @@ __device__ __forceinline__ void wide_leaf(const Scene& S, Trav& t, double t_min,
                                           Side& side) {
   if (t.pend >= 0) {
     const rt_node* n = &S.leaves[t.pend];  // (pend holds the leaf table slot)
-    trav_leaf<F>(S, t, n, n->c, t_min, cnt, g, side, false);
+    trav_leaf<F>(S, t, n, t.pend | kSlotTag, t_min, cnt, g, side, false);
     t.pend = -1;
   }
   trav_postpone(t, stk, stride);
@@ -911,8 +915,11 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
 // `r` is the world ray. Callers check `tie` first and re-walk with trav_restart_ref.
 template <unsigned F>
 __device__ __forceinline__ bool leaf_record(const Scene& S, const Trav& t, const Ray& r, double t_min, Hit& h) {
+  // (a leaf of the 4-wide walk: its record from the leaf table)
+  const bool slot = (F & F_WIDE) && (t.best_node & kSlotTag);
+  const rt_node* n = slot ? &S.leaves[t.best_node & ~kSlotTag] : &S.nodes[t.best_node];
   if constexpr ((F & F_INST) != 0)
-    if (t.best_sub == kSubChain) return chain_hit<F>(S, t.best_node, r, t_min, t.best_tmax, h);
+    if (t.best_sub == kSubChain) return chain_hit<F>(S, slot ? n->c : t.best_node, r, t_min, t.best_tmax, h);
   if constexpr ((F & F_MEDIA) != 0)
     if (t.best_sub == kSubMedium) {
       h.t = t.closest;
@@ -924,7 +931,7 @@ __device__ __forceinline__ bool leaf_record(const Scene& S, const Trav& t, const
       h.mat = S.nodes[t.best_node].b;
       return true;
     }
-  prim_record<F>(S, &S.nodes[t.best_node], t.best_sub, r, t.closest, h);
+  prim_record<F>(S, n, t.best_sub, r, t.closest, h);
   return true;
 }
 template <unsigned F>
