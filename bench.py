@@ -127,6 +127,36 @@ def pmc_traffic(args, kernel_ms):
         f"live kernel time; profiled launch {s['avg_duration_s'] * 1e3:.1f} ms")
 
 
+def pmc_valu(args):
+    """The binding roof's view (VALU issue) from the same PMC summary: the share of the SIMDs'
+    cycles the render kernel's vector instructions occupy, at 2 cycles per wave64 instruction on a
+    SIMD-32 and 4 for fp64 ones (MI355X_MICROARCH.md: v_fma_f32 2 cycles; the fp64 vector peak is
+    half the fp32 one), over the profiled launch's SIMD-cycles (1024 SIMDs x the measured clock),
+    and the lane utilisation of the issued instructions."""
+    path = args.traffic_json or _latest_profile(f"pmc_{args.config}.json")
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        s = json.load(f)
+    c, dur = s.get("counters_per_dispatch", {}), s.get("avg_duration_s")
+    need = ("SQ_INSTS_VALU", "GRBM_GUI_ACTIVE", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+            "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")
+    if not dur or any(k not in c for k in need):
+        return None
+    f64 = sum(c[k] for k in need[2:])
+    clock = c["GRBM_GUI_ACTIVE"] / 8 / dur  # GRBM_GUI_ACTIVE sums the 8 XCDs
+    busy = (2 * (c["SQ_INSTS_VALU"] - f64) + 4 * f64) / (1024 * clock * dur)
+    out = {"bound": "valu", "achieved": round(c["SQ_INSTS_VALU"] / dur / 1e9, 2),
+           "peak": round(1024 * clock / 2 / 1e9, 2), "unit": "G wave-instr/s",
+           "frac": round(busy, 4), "fp64_share": round(f64 / c["SQ_INSTS_VALU"], 4),
+           "clock_ghz": round(clock / 1e9, 3),
+           "lane_utilisation": round(s.get("derived", {}).get("valu_lane_utilisation", 0.0), 4),
+           "source": os.path.relpath(path, ROOT),
+           "note": "frac = SIMD cycles occupied by vector issue (2 per wave64 instruction, 4 per fp64 one) "
+                   "over the profiled launch; achieved/peak count wave instructions at the 2-cycle rate"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -298,7 +328,8 @@ def main():
                                "note": "achieved = algorithmic scene-record bytes (4-wide nodes, leaves, materials) "
                                        "per sample, device-counted by the counting build of the same launch, over "
                                        "the kernel time; they are served from LDS and L2, not HBM (traffic = the "
-                                       "PMC-measured HBM bytes). The binding roof is VALU issue (see fp64/fp32)"}
+                                       "PMC-measured HBM bytes). The binding roof is VALU issue (see valu_roofline)"}
+            out["valu_roofline"] = pmc_valu(args)
             out["fp64"] = {"achieved_tflops": round(fl, 3), "peak_tflops": FP64_PEAK_TFLOPS,
                            "frac": round(fl / FP64_PEAK_TFLOPS, 5), "flops_per_sample": round(flops_per_sample, 1)}
             f32 = sum(FLOPS32[k] * per.get(k, 0) for k in FLOPS32)
