@@ -1136,7 +1136,10 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   if (const char* ce = std::getenv("RTAMD_CHUNK")) A.chunk = std::max(1, std::min(p->spp, std::atoi(ce)));
   A.chunks = (p->spp + A.chunk - 1) / A.chunk;
   A.work_total = slab * A.chunks;
-  if (A.work_total >= (1ll << 32)) return invalid("image too large: more than 2^32 work-items per shard");
+  // (work-item indices are 32-bit on the device, and wave claims may run up to one batch per wave
+  // past the end: keep 2^24 of headroom)
+  if (A.work_total >= (1ll << 32) - (1ll << 24))
+    return invalid("image too large: more than 2^32 - 2^24 work-items per shard");
   A.div_tp = make_udiv((uint32_t)(A.tile * A.tile));
   A.div_tile = make_udiv((uint32_t)(A.tile * A.tile * A.chunks));
   A.div_tiles_x = make_udiv((uint32_t)A.tiles_x);
