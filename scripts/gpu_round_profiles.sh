@@ -14,6 +14,6 @@ for c in "${cfgs[@]}"; do
   esac
   steps+=(bench_$c 400 "python -u bench.py $b > gpurun_out/${tag}_bench_$c.json"
           stats_$c 300 "cd /tmp && rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/gpurun_out/stats_$c -o $c -- python3 $PWD/bench.py $s --no-cpu-baseline --no-work")
-  [ "$c" = c2 ] && steps+=(pmc_c2 600 "scripts/pmc_passes.sh gpurun_out/pmc_c2 --config c2")
+  case $c in c2) steps+=(pmc_c2 600 "scripts/pmc_passes.sh gpurun_out/pmc_c2 --config c2");; c5) steps+=(pmc_c5 600 "scripts/pmc_passes.sh gpurun_out/pmc_c5 --config c5 --spp 16");; esac
 done
 scripts/gpu_steps.sh "${steps[@]}"
