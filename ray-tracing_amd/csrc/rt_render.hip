@@ -1176,7 +1176,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   // claims together never exceed 1/16 of what is left.
   {
     const char* be = std::getenv("RTAMD_BATCH");
-    A.batch = be ? std::max(1, std::min(4096, std::atoi(be))) : 256;
+    A.batch = be ? std::max(1, std::min(4096, std::atoi(be))) : 1024;
     const double waves = (double)c->cu_count * 4 * 4;  // at most 4 waves per SIMD
     A.batch_per_item = (float)(1.0 / (16.0 * waves));
   }
