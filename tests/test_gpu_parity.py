@@ -313,17 +313,22 @@ def test_skewed_spine_world_walks(gpu_ctx, wide, monkeypatch):
 
 @pytest.mark.parametrize("name,cam", [("random_book_one", "random_scene"), ("next_week_final", "next_week")])
 def test_work_claims_do_not_change_the_image(gpu_ctx, name, cam, monkeypatch):
-    """Work-items are claimed per wave in batches (RTAMD_BATCH, default 256, tapering as the frame
+    """Work-items are claimed per wave in batches (RTAMD_BATCH, default 1024, tapering as the frame
     runs out): which lane renders which (pixel, chunk) changes, the chunk sums and their order do
-    not, so the image is identical for any batch size."""
+    not, so the image is identical for any batch size. Every item must be rendered exactly once:
+    each render follows one with another seed (a dropped item would leave that render's chunk sum
+    in the buffer), and the counting build counts every sample."""
     earth = np.load(_earth_path())["rgb"] if name == "next_week_final" else None
     sc, _ = _scene(name, earth=earth)
     c = rtamd.camera(cam, 128, 96)
     gpu_ctx.upload(sc)
     p = rtamd.make_params(128, 96, 24, 50, rtamd.RT_RNG_PHILOX, seed=17)
+    other = rtamd.make_params(128, 96, 24, 50, rtamd.RT_RNG_PHILOX, seed=99)
     out = []
-    for b in ("1", "7", "256"):
+    for b in ("1", "7", "256", "4096"):
         monkeypatch.setenv("RTAMD_BATCH", b)
+        gpu_ctx.render(c, other)
         out.append(gpu_ctx.render(c, p, linear=True))
+        assert gpu_ctx.render_work(c, p)["samples"] == 128 * 96 * 24
     for rgb, lin, _ in out[1:]:
         assert np.array_equal(rgb, out[0][0]) and np.array_equal(lin, out[0][1], equal_nan=True)
