@@ -1004,11 +1004,15 @@ constexpr size_t kLdsBudget = 160 * 1024 - 16 * 8;
 // Kernel variants: spheres-only (configs 1, 2, 5), Cornell-like (rects, instances, lights), full.
 constexpr unsigned kVarSpheres = 0u;
 constexpr unsigned kVarCornell = F_RECT | F_INST | F_LIGHTS;
+// the full variant without light sampling (lights Unhittable: next_week_final, the textured
+// scenes), whose Lambertian scatter needs no lights-tree code
+constexpr unsigned kVarFullDark = F_ALL & ~F_LIGHTS;
 unsigned variant_for(unsigned f) {
   if ((f & ~kVarSpheres) == 0) return kVarSpheres;
   if ((f & ~kVarCornell) == 0) return kVarCornell;
-  return F_ALL;
+  return (f & F_LIGHTS) ? F_ALL : kVarFullDark;
 }
+bool is_full(unsigned var) { return (var & F_FRAMES) != 0; }
 // Occupancy target (waves per SIMD) of the render kernel; RTAMD_WAVES overrides (1..4) for A/B
 // measurements. The defaults (launch_philox) are measured.
 int waves_target(int dflt) {
@@ -1058,18 +1062,22 @@ const void* pick(int loop, bool lds, int w, bool count, bool leaf_lds) {
   if (w == 4) return (const void*)render_philox<V, 4>;
   return (const void*)render_philox<V, 1>;
 }
+// full variants (media, frames, textures, motion): ray replacement over the caller's tree in the
+// reference's order (loop 1), or the per-sample loop (loop 0)
+template <unsigned V>
+const void* pick_full(int loop, bool lds, int w, bool count) {
+  if (count) return loop ? (const void*)render_philox2<V | F_COUNT, 1> : (const void*)render_philox<V | F_COUNT, 1>;
+  if (loop) {
+    if (lds) return w >= 3 ? (const void*)render_philox2_lds<V, 3> : (const void*)render_philox2_lds<V, 2>;
+    return w >= 3 ? (const void*)render_philox2<V, 3> : (const void*)render_philox2<V, 2>;
+  }
+  return w >= 2 ? (const void*)render_philox<V, 2> : (const void*)render_philox<V, 1>;
+}
 const void* philox_kernel(unsigned var, int loop, bool lds, int w, bool count, bool leaf_lds = false) {
   if (var == kVarSpheres) return pick<kVarSpheres>(loop, lds, w, count, leaf_lds);
   if (var == kVarCornell) return pick<kVarCornell>(loop, lds, w, count, leaf_lds);
-  // full variant (media, frames, textures, motion): ray replacement over the caller's tree in the
-  // reference's order (loop 1), or the per-sample loop (loop 0)
-  if (count)
-    return loop ? (const void*)render_philox2<F_ALL | F_COUNT, 1> : (const void*)render_philox<F_ALL | F_COUNT, 1>;
-  if (loop) {
-    if (lds) return w >= 3 ? (const void*)render_philox2_lds<F_ALL, 3> : (const void*)render_philox2_lds<F_ALL, 2>;
-    return w >= 3 ? (const void*)render_philox2<F_ALL, 3> : (const void*)render_philox2<F_ALL, 2>;
-  }
-  return w >= 2 ? (const void*)render_philox<F_ALL, 2> : (const void*)render_philox<F_ALL, 1>;
+  if (var == kVarFullDark) return pick_full<kVarFullDark>(loop, lds, w, count);
+  return pick_full<F_ALL>(loop, lds, w, count);
 }
 bool env_off(const char* name) {
   const char* e = std::getenv(name);
@@ -1181,7 +1189,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
     A.batch_per_item = (float)(1.0 / (16.0 * waves));
   }
   A.trav_stop = stop_env ? std::max(0, std::min(63, std::atoi(stop_env)))
-                         : (c->n_nodes > 20000 || variant_for(c->features) == F_ALL ? 16 : 8);
+                         : (c->n_nodes > 20000 || is_full(variant_for(c->features)) ? 16 : 8);
   const char* leaf_env = std::getenv("RTAMD_LEAF_STOP");
   // leaf steps once <= that many lanes still seek their first leaf (measured: C2 212.6 ms at 6-8/64
   // vs 219.7 at 0 and 232 without postponement; C5 (16 spp) 219.9 ms at 16/64 vs 326 at 0)
@@ -1198,18 +1206,18 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   const char* wenv = std::getenv("RTAMD_WIDE");
   const bool want_wide = wenv ? wenv[0] != '0' : c->rebuilt_bvh;
   // (the full variant has no 4-wide instantiation: its media-free worlds walk the binary tree)
-  const bool wide = replace && c->d_wnodes && !(p->flags & RT_FLAG_REFERENCE_CULL) && want_wide && var != F_ALL;
+  const bool wide = replace && c->d_wnodes && !(p->flags & RT_FLAG_REFERENCE_CULL) && want_wide && !is_full(var);
   const int loop = wide ? 2 : (replace ? 1 : 0);
   // waves per SIMD (measured): spheres 4 when the LDS-staged kernel fits at 4 (C2 158.4 ms vs
   // 166.6 at 3, 203.2 at 2), else 3 (C5 186.7 ms vs 228.5 at 4, -15 % at 2); Cornell-like on the
   // replacement loop 3 (C3 359.6 ms vs 374.3 at 4, 453.3 at 2), 1 on the per-sample loop; full
   // variant on the replacement loop 3 (C4 at 100 spp: 90.9 vs 87.5 Msamples/s at 2), on the
   // per-sample loop 2 despite 784 B/lane of scratch (C4 35.2 vs 23.4 at 1 wave, 9.1 at 3)
-  int waves = (var == kVarSpheres || loop) ? waves_target(3) : waves_target(var == F_ALL ? 2 : 1);
+  int waves = (var == kVarSpheres || loop) ? waves_target(3) : waves_target(is_full(var) ? 2 : 1);
   const int side_ints = (var & F_FRAMES) && loop == 1 ? kSideInts : 0;  // Side slots after the stacks
   // LDS-staged kernel when the traversal's node array plus the stacks fit one CU's 160 KiB
   // (RTAMD_LDS=0 disables it for A/B runs).
-  if (!count && !env_off("RTAMD_LDS") && (var != F_ALL || loop)) {
+  if (!count && !env_off("RTAMD_LDS") && (!is_full(var) || loop)) {
     const int entries = wide ? c->wide_stack_need + 3 : c->stack_need + 2;  // (wide_node writes 3 slots)
     const int items = wide ? c->n_wnodes : c->n_nodes;
     const size_t rec = wide ? sizeof(rt_wnode) : sizeof(rt_node);
