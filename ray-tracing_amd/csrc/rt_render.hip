@@ -978,7 +978,7 @@ int check_params(const rt_render_params* p) {
     return invalid("width/height/spp must be positive and max_depth >= 0");
   if (p->rng_mode != RT_RNG_EXACT && p->rng_mode != RT_RNG_PHILOX) return invalid("unknown rng_mode");
   const int tile = p->tile ? p->tile : 16;
-  if (tile <= 0 || tile % 8) return invalid("tile must be a positive multiple of 8");
+  if (tile <= 0 || tile % 8 || tile > 256) return invalid("tile must be a multiple of 8 in [8, 256]");
   if (p->shard_count < 0 || (p->shard_count > 0 && (p->shard_rank < 0 || p->shard_rank >= p->shard_count)) ||
       (p->shard_count <= 1 && p->shard_rank != 0))
     return invalid("bad shard_rank/shard_count");
@@ -1481,6 +1481,7 @@ int rt_assemble_async(rt_ctx* c, const rt_render_params* p, const uint8_t* d_sla
   long long tt, ps, sp;
   geometry(p, tile, tiles_x, tt, ps, sp);
   const long long n = (long long)p->width * p->height;
+  HIPCHK(hipSetDevice(c->device));  // (the caller's current device may be another ctx's)
   hipLaunchKernelGGL(assemble<uint8_t>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_slabs,
                      d_image, p->width, p->height, tile, tiles_x, p->shard_count > 0 ? p->shard_count : 1, sp);
   HIPCHK(hipGetLastError());
@@ -1496,6 +1497,7 @@ int rt_assemble_linear_async(rt_ctx* c, const rt_render_params* p, const double*
   long long tt, ps, sp;
   geometry(p, tile, tiles_x, tt, ps, sp);
   const long long n = (long long)p->width * p->height;
+  HIPCHK(hipSetDevice(c->device));
   hipLaunchKernelGGL(assemble<double>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_slabs,
                      d_image, p->width, p->height, tile, tiles_x, p->shard_count > 0 ? p->shard_count : 1, sp);
   HIPCHK(hipGetLastError());

@@ -41,8 +41,10 @@ def test_struct_sizes_match_header():
 def test_param_validation_without_gpu():
     with pytest.raises(rtamd.RTError):
         rtamd.shard_geometry(rtamd.make_params(0, 10, 1, 1))
-    with pytest.raises(rtamd.RTError):
-        rtamd.shard_geometry(rtamd.make_params(10, 10, 1, 1, tile=12))
+    for tile in (12, -8, 264, 65536):  # (tile*tile must stay a 32-bit work-item count)
+        with pytest.raises(rtamd.RTError):
+            rtamd.shard_geometry(rtamd.make_params(10, 10, 1, 1, tile=tile))
+    assert rtamd.shard_geometry(rtamd.make_params(10, 10, 1, 1, tile=256))[0] == 1
     with pytest.raises(rtamd.RTError):
         rtamd.shard_geometry(rtamd.make_params(10, 10, 1, 1, shard_rank=2, shard_count=2))
     for count in (0, 1):  # an unsharded launch has only rank 0 (a stray rank shifted the tile map)
