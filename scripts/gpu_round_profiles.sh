@@ -10,6 +10,7 @@ for c in "${cfgs[@]}"; do
   case $c in
     c2) b="--steps 5"; s="--steps 3";;
     c5) b="--config c5 --spp 16 --steps 3"; s="--config c5 --spp 16 --steps 2";;
+    c1) b="--config c1 --steps 20 --warmup 3"; s="--config c1 --steps 20 --warmup 3";;  # (launch-bound: warm up)
     *)  b="--config $c --steps 1 --warmup 0"; s="--config $c --steps 1 --warmup 0";;
   esac
   steps+=(bench_$c 400 "python -u bench.py $b > gpurun_out/${tag}_bench_$c.json"
