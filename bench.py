@@ -108,21 +108,33 @@ def _latest_profile(suffix):
     return path
 
 
+def default_selection(args):
+    """True when this run launches the default kernel selection of its config (no RTAMD_* knobs, no
+    culling / BVH / spp / tile overrides): only then does a committed PMC summary describe it."""
+    return not any(k.startswith("RTAMD_") for k in os.environ) and not (
+        args.nan_cull or args.reference_cull or args.reference_bvh or args.spp or args.tile != 16)
+
+
+def _pmc_summary(args):
+    path = args.traffic_json or _latest_profile(f"pmc_{args.config}.json")
+    if not path or not os.path.exists(path) or not (default_selection(args) or args.traffic_json):
+        return None, path
+    with open(path) as f:
+        return json.load(f), path
+
+
 def pmc_traffic(args, kernel_ms):
     """HBM traffic of the render kernel from the committed rocprofv3 PMC summary of the same
     config (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE, bytes per launch), as GB/s over
-    this run's live kernel time. None when no summary matches the launched kernel selection."""
-    path = args.traffic_json or _latest_profile(f"pmc_{args.config}.json")
-    default_sel = not any(k.startswith("RTAMD_") for k in os.environ) and not (
-        args.nan_cull or args.reference_cull or args.reference_bvh or args.spp or args.tile != 16)
-    if not os.path.exists(path) or not (default_sel or args.traffic_json):
-        return None, "no PMC summary for this kernel selection"
-    with open(path) as f:
-        s = json.load(f)
+    this run's live kernel time, and the bytes per launch. None when no summary matches the launched
+    kernel selection."""
+    s, path = _pmc_summary(args)
+    if s is None:
+        return None, None, "no PMC summary for this kernel selection"
     b = s.get("derived", {}).get("hbm_bytes")
     if b is None:
-        return None, f"{os.path.basename(path)} has no FETCH_SIZE/WRITE_SIZE"
-    return round(b / (kernel_ms * 1e-3) / 1e9, 3), (
+        return None, None, f"{os.path.basename(path)} has no FETCH_SIZE/WRITE_SIZE"
+    return round(b / (kernel_ms * 1e-3) / 1e9, 3), round(b), (
         f"{os.path.relpath(path, ROOT)}: {b / 1e6:.1f} MB/launch HBM (FETCH_SIZE x2 + WRITE_SIZE) over the "
         f"live kernel time; profiled launch {s['avg_duration_s'] * 1e3:.1f} ms")
 
@@ -132,12 +144,11 @@ def pmc_valu(args):
     cycles the render kernel's vector instructions occupy, at 2 cycles per wave64 instruction on a
     SIMD-32 and 4 for fp64 ones (MI355X_MICROARCH.md: v_fma_f32 2 cycles; the fp64 vector peak is
     half the fp32 one), over the profiled launch's SIMD-cycles (1024 SIMDs x the measured clock),
-    and the lane utilisation of the issued instructions."""
-    path = args.traffic_json or _latest_profile(f"pmc_{args.config}.json")
-    if not path or not os.path.exists(path):
+    and the lane utilisation of the issued instructions. None unless the run launches the kernel
+    selection the summary was profiled on (default_selection)."""
+    s, path = _pmc_summary(args)
+    if s is None:
         return None
-    with open(path) as f:
-        s = json.load(f)
     c, dur = s.get("counters_per_dispatch", {}), s.get("avg_duration_s")
     need = ("SQ_INSTS_VALU", "GRBM_GUI_ACTIVE", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
             "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")
@@ -151,10 +162,47 @@ def pmc_valu(args):
            "frac": round(busy, 4), "fp64_share": round(f64 / c["SQ_INSTS_VALU"], 4),
            "clock_ghz": round(clock / 1e9, 3),
            "lane_utilisation": round(s.get("derived", {}).get("valu_lane_utilisation", 0.0), 4),
+           "kernels": s.get("kernels"), "profiled_launch_ms": round(dur * 1e3, 3),
            "source": os.path.relpath(path, ROOT),
            "note": "frac = SIMD cycles occupied by vector issue (2 per wave64 instruction, 4 per fp64 one) "
                    "over the profiled launch; achieved/peak count wave instructions at the 2-cycle rate"}
     return out
+
+
+def sample_chunk(pixels, spp):
+    """rt_sample_chunk (include/rt.h): samples per tier-B work-item."""
+    fill = (pixels * spp + (1 << 20) - 1) >> 20
+    ch = max(8, (spp + 63) // 64)
+    ch = min(ch, spp, fill)
+    return max(1, ch)
+
+
+def algorithmic_offchip_bytes(cfg, p, scene):
+    """Off-chip bytes the render kernel must move per launch, for this rank's slab: the chunk sums it
+    writes (slab pixels x chunks x 24 B), the RGB8 slab combine_chunks writes (3 B per pixel), and the
+    scene records read once (nodes incl. the device rebuild, 4-wide nodes, leaves, materials,
+    textures, Perlin tables, image pool)."""
+    _, _, slab = rtamd.shard_geometry(p)
+    chunks = -(-cfg["spp"] // sample_chunk(cfg["W"] * cfg["H"], cfg["spp"]))
+    d = scene.desc
+    try:
+        n_nodes = rtamd.rebuilt_scene(scene).desc.n_nodes
+    except rtamd.RTError:
+        n_nodes = d.n_nodes
+    scene_b = (64 * n_nodes + 24 * d.n_materials + 48 * d.n_textures + 9216 * d.n_perlins + d.image_pool_bytes)
+    out = {"chunk_sums": int(slab * chunks * 24), "image": int(slab * 3), "scene": int(scene_b)}
+    out["total"] = sum(out.values())
+    return out
+
+
+def cpu_threads(args):
+    """Threads for the CPU baseline: --cpu-threads if given, else the CPUs this process may run on
+    (os.sched_getaffinity), capped by OMP_NUM_THREADS when the environment sets it (the GPU box
+    sets it to this job's CPU share, 16 per GPU, while nproc shows the whole machine)."""
+    aff = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS")
+    n = args.cpu_threads or min(aff, int(env) if env and env.isdigit() else aff)
+    return n, {"affinity": aff, "nproc": os.cpu_count(), "omp_env": env}
 
 
 def main():
@@ -170,7 +218,8 @@ def main():
                     help="traverse the reference's makeBVH world tree (default: SAH rebuild over the same leaves)")
     ap.add_argument("--spp", type=int, default=0, help="override spp (sampled runs of the big configs; not the metric)")
     ap.add_argument("--tile", type=int, default=16)
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (default: the affinity CPU count, capped by OMP_NUM_THREADS)")
     ap.add_argument("--cpu-spp", type=int, default=0,
                     help="spp cap of the bounded CPU sample (default min(spp, 40M/(W*H)); a probe sizes the sample to ~10 s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -212,60 +261,48 @@ def main():
         rtamd.RT_FLAG_REFERENCE_CULL if args.reference_cull else 0)
     p = rtamd.make_params(cfg["W"], cfg["H"], cfg["spp"], cfg["depth"], rtamd.RT_RNG_PHILOX, seed=1024,
                           flags=flags, tile=args.tile, shard_rank=rank, shard_count=world)
-    _, _, slab_px = rtamd.shard_geometry(p)
     dev = torch.device("cuda", local)
-    slab = torch.zeros((slab_px, 3), dtype=torch.uint8, device=dev)
-    slabs = torch.zeros((world, slab_px, 3), dtype=torch.uint8, device=dev)
-    image = torch.zeros((cfg["H"], cfg["W"], 3), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
-
-    def step():
-        ctx.render_shard_async(cam, p, slab.data_ptr(), 0, stream.cuda_stream)
-        if world > 1:
-            if args.dist_backend == "nccl":
-                dist.all_gather_into_tensor(slabs, slab)  # RCCL over xGMI
-            else:
-                host = slab.cpu()
-                parts = [torch.empty_like(host) for _ in range(world)]
-                dist.all_gather(parts, host)
-                slabs.copy_(torch.stack(parts))
-            src = slabs
-        else:
-            src = slab
-        if rank == 0:
-            ctx.assemble_async(p, src.data_ptr(), image.data_ptr(), stream.cuda_stream)
+    from rtamd.frame import ShardedFrame, device_assembler, device_renderer
+    frame = ShardedFrame(p, world, rank, dev, args.dist_backend,
+                         render=device_renderer(ctx, cam, stream.cuda_stream),
+                         assemble=device_assembler(ctx, stream.cuda_stream))
 
     # device-measured work of this exact launch (counting build, outside the timed region)
     work = ctx.render_work(cam, p) if not args.no_work else None
 
     for i in range(args.warmup):
-        step()
+        frame.step()
         torch.cuda.synchronize()
         log(f"[rank {rank}] warmup {i + 1}/{args.warmup} done")
+    frame.finish()
+    frame.timings.clear()
 
-    kernel_ms = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step()
-        kernel_ms.append(ctx.last_kernel_ms())  # HIP events around the render launch, same stream
-        log(f"[rank {rank}] step {i + 1}/{args.steps}: kernel {kernel_ms[-1]:.1f} ms")
+        frame.step(kernel_ms=ctx.last_kernel_ms)  # (HIP events around the render launch, same stream)
+        log(f"[rank {rank}] step {i + 1}/{args.steps}: kernel {frame._ev[-1][1]:.1f} ms")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    frame.finish()
+    mine = frame.summary()  # this rank's mean kernel / all-gather / assemble ms
+    per_rank = [mine]
     if world > 1:
         rdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
         t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        km = torch.tensor([float(np.mean(kernel_ms))], dtype=torch.float64, device=rdev)
-        dist.all_reduce(km, op=dist.ReduceOp.MAX)
-        kernel_avg = float(km.item())
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
+        kernel_avg = max(r["kernel_ms"] for r in per_rank)
     else:
-        kernel_avg = float(np.mean(kernel_ms))
+        kernel_avg = mine["kernel_ms"]
+    image = frame.image
 
     if rank == 0:
         samples_frame = cfg["W"] * cfg["H"] * cfg["spp"]
@@ -297,12 +334,20 @@ def main():
         if not args.no_cpu_baseline and world == 1:  # the CPU leg is timed at N=1 only
             if not args.cpu_spp:
                 args.cpu_spp = max(1, min(cfg["spp"], round(40e6 / (cfg["W"] * cfg["H"]))))
-            v, dt, counters, what = cpu_baseline(cfg, scene, cam, args.cpu_threads, args.cpu_spp)
-            cb = {"value": round(v, 4), "unit": "Msamples/s", "cores": args.cpu_threads, "kind": "port",
-                  "cpu": cpu_model(),
+            threads, cores = cpu_threads(args)
+            v, dt, counters, what = cpu_baseline(cfg, scene, cam, threads, args.cpu_spp)
+            cb = {"value": round(v, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+                  "affinity_cpus": cores["affinity"], "nproc": cores["nproc"],
+                  "omp_num_threads_env": cores["omp_env"], "cpu": cpu_model(),
                   "sample": f"{what} (tier-B streams of the same frame), {dt:.1f} s, oracle/oracle.c fp64 glibc "
-                            f"-O2 OpenMP"}
+                            f"-O2 OpenMP, {threads} threads"}
         out["cpu_baseline"] = cb
+        out["timing_per_rank_ms"] = [{k: round(v, 3) for k, v in r.items()} for r in per_rank]
+        if world > 1:
+            out["dist"] = {"backend": args.dist_backend, "world_size": dist.get_world_size(),
+                           "slab_bytes_per_rank": int(frame.slab.numel()),
+                           "note": "per rank: render kernel (HIP events), all-gather and assemble (events on the "
+                                   "launch stream) means over the timed steps; assemble runs on rank 0 only"}
         if work:
             n = max(1, work["samples"])
             out["phase_split"] = {k: round(v, 4) for k, v in work.pop("phase_split").items()}
@@ -316,24 +361,39 @@ def main():
             per = {k: work[k] / n for k in work}
             bytes_per_sample = sum(BYTES[k] * per[k] for k in BYTES) + 3.0 / cfg["spp"]
             flops_per_sample = sum(FLOPS[k] * per[k] for k in FLOPS)
+            f32 = sum(FLOPS32[k] * per.get(k, 0) for k in FLOPS32)
             samples_per_launch = samples_frame / world
-            achieved = bytes_per_sample * samples_per_launch / (kernel_avg * 1e-3) / 1e9
-            fl = flops_per_sample * samples_per_launch / (kernel_avg * 1e-3) / 1e12
-            traffic, tnote = pmc_traffic(args, kernel_avg)
-            out["roofline"] = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                               "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                               "traffic_note": tnote,
-                               "kernel_ms": round(kernel_avg, 3),
-                               "bytes_per_sample": round(bytes_per_sample, 2),
-                               "note": "achieved = algorithmic scene-record bytes (4-wide nodes, leaves, materials) "
-                                       "per sample, device-counted by the counting build of the same launch, over "
-                                       "the kernel time; they are served from LDS and L2, not HBM (traffic = the "
-                                       "PMC-measured HBM bytes). The binding roof is VALU issue (see valu_roofline)"}
+            secs = kernel_avg * 1e-3
+            fl = flops_per_sample * samples_per_launch / secs / 1e12
+            fl32 = f32 * samples_per_launch / secs / 1e12
+            # fp64-equivalent rate: an fp32 op costs half an fp64 one at the vector peaks (157.3 vs 78.6 TF)
+            eq = fl + fl32 * FP64_PEAK_TFLOPS / FP32_PEAK_TFLOPS
+            traffic, tbytes, tnote = pmc_traffic(args, kernel_avg)
+            off = algorithmic_offchip_bytes(cfg, p, scene)
+            out["roofline"] = {
+                "bound": "fp64-valu", "achieved": round(eq, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(eq / FP64_PEAK_TFLOPS, 5),
+                "traffic": traffic, "traffic_unit": "GB/s", "traffic_bytes_per_launch": tbytes,
+                "algorithmic_offchip_bytes": off,
+                "traffic_over_algorithmic": round(tbytes / off["total"], 3) if tbytes else None,
+                "traffic_note": tnote,
+                "kernel_ms": round(kernel_avg, 3),
+                "flops_per_sample": {"fp64": round(flops_per_sample, 1), "fp32": round(f32, 1)},
+                "note": "achieved = algorithmic fp64 flops per sample + fp32 flops at half weight (lower-bound "
+                        "op counts per device-counted unit of work: box / leaf / instance tests, segments, "
+                        "4-wide nodes; bench.py FLOPS), x samples per launch / the render kernel's HIP-event "
+                        "time, against the fp64 vector peak: frac <= 1 by construction. The path is bound by "
+                        "VALU issue under divergence and latency (valu_roofline: the PMC view), not by HBM: "
+                        "traffic = PMC HBM bytes of the same kernel selection (FETCH_SIZE x2 + WRITE_SIZE) "
+                        "next to the algorithmic off-chip bytes (chunk sums, image, scene records read once)"}
+            out["scene_record_stream"] = {
+                "bytes_per_sample": round(bytes_per_sample, 2),
+                "gbs": round(bytes_per_sample * samples_per_launch / secs / 1e9, 2),
+                "note": "algorithmic scene-record bytes per sample (4-wide nodes, leaves, materials) over the "
+                        "kernel time: served from LDS and L2, so not an HBM figure"}
             out["valu_roofline"] = pmc_valu(args)
             out["fp64"] = {"achieved_tflops": round(fl, 3), "peak_tflops": FP64_PEAK_TFLOPS,
                            "frac": round(fl / FP64_PEAK_TFLOPS, 5), "flops_per_sample": round(flops_per_sample, 1)}
-            f32 = sum(FLOPS32[k] * per.get(k, 0) for k in FLOPS32)
-            fl32 = f32 * samples_per_launch / (kernel_avg * 1e-3) / 1e12
             out["fp32"] = {"achieved_tflops": round(fl32, 3), "peak_tflops": FP32_PEAK_TFLOPS,
                            "frac": round(fl32 / FP32_PEAK_TFLOPS, 5), "flops_per_sample": round(f32, 1)}
             out["work_per_sample"] = {k: round(v, 3) for k, v in per.items() if k != "samples"}

@@ -202,6 +202,12 @@ static inline int rt_sample_chunk(int64_t pixels, int spp) {
 #define RT_FLAG_REFERENCE_CULL 2u /* cull BVH boxes with the reference's per-axis test only
                                (src/Lib.hs:798-814). Default: that test AND the joint slab test,
                                which only prunes boxes that cannot hold a hit. */
+#define RT_FLAG_NAN_ZERO 4u /* tier B, parity diagnostic (NOT the reference's semantics): a sample
+                               contribution channel that is NaN is added as 0, so that the finite
+                               part of every sample reaches the average. The reference's Lambertian
+                               light-mixture quirk makes most pixels of the bench frames NaN (C2 mid
+                               rows, all of C4 at 1000 spp); with this flag the same launches carry
+                               every sample's finite colour to a comparable output. */
 
 typedef struct rt_render_params {
     int32_t width;
@@ -300,6 +306,10 @@ int rt_camera_named(int cam_id, int width, int height, rt_camera* out);
 /* P3 PPM text exactly as app/Main.hs:59-61 + printRow/showRow (src/Lib.hs:299-305).
  * Writes at most cap bytes; *out_len = bytes required. */
 int rt_write_ppm(const uint8_t* rgb, int width, int height, char* buf, size_t cap, size_t* out_len);
+/* Float dump of the per-pixel averages (rt_render's out_linear, H*W*3 doubles, top row first) as PFM:
+ * "PF\n<W> <H>\n-1.0\n" + little-endian float32 RGB, bottom row first (the PFM order); f64 != 0
+ * writes doubles under the header "PF64" instead (lossless). Same buffer protocol as rt_write_ppm. */
+int rt_write_pfm(const double* linear, int width, int height, int f64, char* buf, size_t cap, size_t* out_len);
 
 /* ------------------------------------------------------------------ device path */
 typedef struct rt_ctx rt_ctx;
@@ -374,6 +384,26 @@ int rt_render_work(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* p,
 
 /* Timing of the last render launch on this ctx (HIP events on the launch stream), ms. */
 int rt_last_kernel_ms(rt_ctx* ctx, double* out_ms);
+
+/* Which kernel the last tier-B render launch on this ctx ran (kernel selection is per scene and
+ * frame: DESIGN.md §3): feature variant (rt_trace.h F_* bits), loop (0 one sample per lane walk,
+ * 1 ray replacement over the binary tree, 2 over the 4-wide tree), LDS-staged scene or global
+ * memory, leaf table in LDS, waves per SIMD the instantiation targets, grid and block size, dynamic
+ * LDS bytes per workgroup, work-items and samples per work-item. */
+typedef struct rt_launch_info {
+    uint32_t variant;
+    int32_t loop;
+    int32_t lds_staged;
+    int32_t leaf_lds;
+    int32_t waves;
+    int32_t grid;
+    int32_t block;
+    int32_t dyn_lds_bytes;
+    int64_t work_items;
+    int32_t chunk;
+    int32_t _pad;
+} rt_launch_info;
+int rt_last_launch(rt_ctx* ctx, rt_launch_info* out);
 
 /*
  * Debug / parity entry: closest hit of n world rays (7 doubles each: origin, direction, time)

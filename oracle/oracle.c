@@ -667,7 +667,11 @@ static V3 render_pixel_exact(const Ctx* c, int x, int y, Rng* g, double* uvbuf) 
 
 /* One pixel, tier B: sample s draws from its own Philox stream; samples summed in sample order
    within fixed chunks, chunk sums in chunk order (include/rt.h, rt_sample_chunk). */
-static V3 render_pixel_philox(const Ctx* c, int x, int y, uint32_t pid, uint64_t seed, int64_t* draws) {
+/* RT_FLAG_NAN_ZERO (parity diagnostic, include/rt.h): a NaN channel of a sample's colour adds 0 */
+static V3 nan_zero(V3 a) { return v3(a.x != a.x ? 0.0 : a.x, a.y != a.y ? 0.0 : a.y, a.z != a.z ? 0.0 : a.z); }
+
+static V3 render_pixel_philox(const Ctx* c, int x, int y, uint32_t pid, uint64_t seed, uint32_t flags,
+                              int64_t* draws) {
     V3 acc = v3(0, 0, 0);
     const int ch = rt_sample_chunk((int64_t)c->width * c->height, c->spp);
     for (int k0 = 0; k0 < c->spp; k0 += ch) {
@@ -687,6 +691,7 @@ static V3 render_pixel_philox(const Ctx* c, int x, int y, uint32_t pid, uint64_t
             double v = ((double)y + rv) / (double)c->height;
             Ray r = get_ray(c, u, v, &g);
             V3 c1 = ray_color(c, r, c->max_depth, &g);
+            if (flags & RT_FLAG_NAN_ZERO) c1 = nan_zero(c1);
             part = vadd(part, c1);
             CNT(c, C_SAMPLES);
         }
@@ -761,7 +766,7 @@ int oracle_render_rows(const rt_scene_desc* scene, const rt_camera* cam, const r
                 int row = row0 + (int)(i / W), x = (int)(i % W);
                 int y = H - 1 - row;
                 uint32_t pid = (uint32_t)((int64_t)row * W + x);
-                V3 a = render_pixel_philox(&c, x, y, pid, p->seed, counters ? &cnt[C_DRAWS] : NULL);
+                V3 a = render_pixel_philox(&c, x, y, pid, p->seed, p->flags, counters ? &cnt[C_DRAWS] : NULL);
                 store_pixel(rgb, linear, i, a);
             }
             if (counters) {

@@ -154,6 +154,11 @@ __device__ __forceinline__ uint8_t scale_color(double x) {
   return f == f ? (uint8_t)(int)f : (uint8_t)0;
 }
 
+// RT_FLAG_NAN_ZERO (parity diagnostic, rt.h): a NaN channel of a sample's colour adds 0
+__device__ __forceinline__ V3 nan_zero(V3 a) {
+  return v3(a.x != a.x ? 0.0 : a.x, a.y != a.y ? 0.0 : a.y, a.z != a.z ? 0.0 : a.z);
+}
+
 __device__ __forceinline__ void store_pixel(const RenderArgs& A, long long idx, V3 avg) {
   A.out_rgb[idx * 3 + 0] = scale_color(avg.x);
   A.out_rgb[idx * 3 + 1] = scale_color(avg.y);
@@ -316,6 +321,7 @@ __device__ __forceinline__ void philox_loop(const RenderArgs& A, const Scene& S,
         blocks += g.pair;
         ++samples;
       }
+      if (A.flags & RT_FLAG_NAN_ZERO) contrib = nan_zero(contrib);
       sum = sum + contrib;
       path = false;
       ++s;
@@ -409,6 +415,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
       blocks += g.pair;
       ++samples;
     }
+    if (A.flags & RT_FLAG_NAN_ZERO) contrib = nan_zero(contrib);
     sum = sum + contrib;
     ++s;
     const bool all_nan = (A.flags & RT_FLAG_NAN_CULL) && sum.x != sum.x && sum.y != sum.y && sum.z != sum.z;
@@ -425,11 +432,11 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
       ++cnt.oslot;
     }
     // ---- shade finished walks, then set up the next walk for every lane that is not walking
-    if (ready && t.tie) {  // exact tie: redo this walk as the reference does
+    if (ready && t.tie && !t.redo) {  // exact tie: redo this walk as the reference does (once)
       ready = false;
       if constexpr ((F & F_COUNT) != 0) ++cnt.ties;
       if constexpr (kRefMixed<F>) g.rewind(walk_mark);  // (the walk's media draws repeat)
-      trav_restart_ref(t, S.world_ref, INFINITY);
+      trav_restart_ref(t, S.world_ref, INFINITY, true);
       walking = true;
     }
     // the next walk's ray: a scattered ray (next segment) or a camera ray (next sample), parked in
@@ -576,12 +583,15 @@ constexpr int lane_ints() {
   return ((F & F_WIDE) ? RT_WSTACK : RT_STACK) + ((F & F_FRAMES) ? kSideInts : 0);
 }
 
+// Global-memory replacement loop: the lane stacks (and Side slots) in dynamic LDS sized by the host
+// for the world's stack bound (`stack_entries` per lane), not for the RT_STACK / RT_WSTACK maxima:
+// the LDS per workgroup then does not cap the occupancy (C4: 54 -> 40 ints per lane, 2.5 -> 3 waves
+// per SIMD).
 template <unsigned F, int WAVES>
-__global__ void __launch_bounds__(RT_BLOCK, WAVES) render_philox2(RenderArgs A) {
-  __shared__ int stk_mem[lane_ints<F>() * RT_BLOCK];
+__global__ void __launch_bounds__(RT_BLOCK, WAVES) render_philox2(RenderArgs A, int stack_entries) {
+  extern __shared__ __attribute__((aligned(16))) int stk_mem[];
   __shared__ uint32_t wave_q[RT_BLOCK / 64][2];
-  constexpr int stack = (F & F_WIDE) ? RT_WSTACK : RT_STACK;
-  philox_loop2<F>(A, A.S, &stk_mem[threadIdx.x], RT_BLOCK, &stk_mem[stack * RT_BLOCK + threadIdx.x],
+  philox_loop2<F>(A, A.S, &stk_mem[threadIdx.x], RT_BLOCK, &stk_mem[stack_entries * RT_BLOCK + threadIdx.x],
                   wave_q[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)]);
 }
 
@@ -721,7 +731,7 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
     walk_until<F>(S, t, walking, tmin, stk, RT_BLOCK, joint != 0, 0, 0, cnt, g, side);
     if (t.tie) {
       if (S.ref_walk) g.rewind(0);  // media draws repeat on the caller's tree
-      trav_restart_ref(t, S.world_ref, tmax);
+      trav_restart_ref(t, S.world_ref, tmax, true);
       while (trav_step<F>(S, t, tmin, stk, RT_BLOCK, joint != 0, cnt, g, side)) {
       }
     }
@@ -796,6 +806,7 @@ struct rt_ctx {
   double* d_partial = nullptr;  // tier-B chunk sums (grown on demand)
   size_t partial_bytes = 0;
   double last_ms = 0.0;
+  rt_launch_info last_launch{};  // rt_last_launch
 };
 
 namespace {
@@ -820,6 +831,25 @@ struct DevBuf {
     if (p) (void)hipFree(p);
   }
 };
+
+// Selects a ctx's device for the duration of a C-ABI call and restores the caller's current device
+// on every return path (a process driving several GPUs from one thread keeps its own selection).
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    err = hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+#define DEVICE_SCOPE(dev)                                  \
+  DeviceGuard _dg(dev);                                    \
+  if (_dg.err != hipSuccess) return hip_fail(_dg.err, "hipSetDevice")
 
 int invalid(const std::string& s) {
   rt::set_error(s);
@@ -1241,6 +1271,8 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
       HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
       int n_items = items;
       void* args[] = {&A, &n_items, (void*)&entries, &n_leaves};
+      c->last_launch = rt_launch_info{var | (loop == 2 ? F_WIDE : 0u), loop, 1, n_leaves > 0, waves, c->cu_count,
+                                      block, (int)bytes, A.work_total, A.chunk, 0};
       HIPCHK(hipEventRecord(c->ev0, st));
       HIPCHK(hipLaunchKernel(fn, dim3(c->cu_count), dim3(block), args, bytes, st));
       HIPCHK(hipEventRecord(c->ev1, st));
@@ -1248,14 +1280,20 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
     }
   }
   const void* fn = philox_kernel(var, loop, false, count ? 1 : waves, count);
+  // replacement loops: lane stacks (+ Side slots) in dynamic LDS, sized for this world's stack bound
+  int entries = wide ? c->wide_stack_need + 3 : c->stack_need + 2;  // (wide_node writes 3 slots)
+  const size_t dyn = loop ? (size_t)(entries + side_ints) * RT_BLOCK * sizeof(int) : 0;
+  if (loop) HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
   int bpc = 1;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, RT_BLOCK, 0));
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, RT_BLOCK, dyn));
   const long long want = (A.work_total + RT_BLOCK - 1) / RT_BLOCK;
   const long long resident = (long long)c->cu_count * std::max(1, bpc);
   const int grid = (int)std::max(1ll, std::min(want, resident));
+  c->last_launch = rt_launch_info{var | (loop == 2 ? F_WIDE : 0u) | (count ? F_COUNT : 0u), loop, 0, 0,
+                                  count ? 1 : waves, grid, RT_BLOCK, (int)dyn, A.work_total, A.chunk, 0};
   HIPCHK(hipEventRecord(c->ev0, st));
-  void* args[] = {&A};
-  HIPCHK(hipLaunchKernel(fn, dim3(grid), dim3(RT_BLOCK), args, 0, st));
+  void* args[] = {&A, &entries};
+  HIPCHK(hipLaunchKernel(fn, dim3(grid), dim3(RT_BLOCK), args, dyn, st));
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev1, st));
   return launch_combine(c, A, st);
@@ -1277,7 +1315,7 @@ int rt_create(int device, rt_ctx** out) {
   int n = 0;
   HIPCHK(hipGetDeviceCount(&n));
   if (device < 0 || device >= n) return invalid("device index out of range");
-  HIPCHK(hipSetDevice(device));
+  DEVICE_SCOPE(device);
   rt_ctx* c = new rt_ctx();
   c->device = device;
   auto init = [c]() -> int {
@@ -1305,7 +1343,7 @@ int rt_create(int device, rt_ctx** out) {
 
 void rt_destroy(rt_ctx* c) {
   if (!c) return;
-  (void)hipSetDevice(c->device);
+  DeviceGuard _dg(c->device);
   free_scene(c);
   (void)hipFree(c->d_counter);
   (void)hipFree(c->d_partial);
@@ -1322,7 +1360,7 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
   if (!c || !din) return invalid("null argument");
   if (din->n_nodes <= 0 || !din->nodes || din->world_root < 0 || din->world_root >= din->n_nodes)
     return invalid("rt_upload_scene: bad node array or world root");
-  HIPCHK(hipSetDevice(c->device));
+  DEVICE_SCOPE(c->device);
   // World-tree rebuild (rt_bvh.cpp) unless the caller or RTAMD_REFERENCE_BVH=1 asks for the
   // reference's own makeBVH tree; never for trees holding media.
   std::vector<rt_node> nodes(din->nodes, din->nodes + din->n_nodes);
@@ -1468,7 +1506,7 @@ int rt_render_shard_async(rt_ctx* c, const rt_camera* cam, const rt_render_param
     return RT_E_STATE;
   }
   if (p->rng_mode != RT_RNG_PHILOX) return invalid("sharded rendering needs RT_RNG_PHILOX (tier B)");
-  HIPCHK(hipSetDevice(c->device));
+  DEVICE_SCOPE(c->device);
   const int shards = p->shard_count > 0 ? p->shard_count : 1;
   return launch_philox(c, cam, p, p->shard_rank, shards, d_rgb, d_lin, (hipStream_t)stream);
 }
@@ -1481,7 +1519,7 @@ int rt_assemble_async(rt_ctx* c, const rt_render_params* p, const uint8_t* d_sla
   long long tt, ps, sp;
   geometry(p, tile, tiles_x, tt, ps, sp);
   const long long n = (long long)p->width * p->height;
-  HIPCHK(hipSetDevice(c->device));  // (the caller's current device may be another ctx's)
+  DEVICE_SCOPE(c->device);  // (the caller's current device may be another ctx's)
   hipLaunchKernelGGL(assemble<uint8_t>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_slabs,
                      d_image, p->width, p->height, tile, tiles_x, p->shard_count > 0 ? p->shard_count : 1, sp);
   HIPCHK(hipGetLastError());
@@ -1497,7 +1535,7 @@ int rt_assemble_linear_async(rt_ctx* c, const rt_render_params* p, const double*
   long long tt, ps, sp;
   geometry(p, tile, tiles_x, tt, ps, sp);
   const long long n = (long long)p->width * p->height;
-  HIPCHK(hipSetDevice(c->device));
+  DEVICE_SCOPE(c->device);
   hipLaunchKernelGGL(assemble<double>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_slabs,
                      d_image, p->width, p->height, tile, tiles_x, p->shard_count > 0 ? p->shard_count : 1, sp);
   HIPCHK(hipGetLastError());
@@ -1517,7 +1555,7 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, cons
     return RT_E_STATE;
   }
   if (p.rng_mode == RT_RNG_EXACT && !col_gens) return invalid("rt_render: tier A needs col_gens (2*width words)");
-  HIPCHK(hipSetDevice(c->device));
+  DEVICE_SCOPE(c->device);
   const long long npx = (long long)p.width * p.height;
   hipStream_t st = c->stream;
   DevBuf img, img_lin, slab_buf, slab_lin, gens;  // freed on every return path
@@ -1576,7 +1614,7 @@ int rt_render_work(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin,
     return RT_E_STATE;
   }
   if (pin->rng_mode != RT_RNG_PHILOX) return invalid("rt_render_work: tier B only");
-  HIPCHK(hipSetDevice(c->device));
+  DEVICE_SCOPE(c->device);
   rt_render_params p = *pin;
   const int shards = p.shard_count > 0 ? p.shard_count : 1;
   int tile, tiles_x;
@@ -1606,6 +1644,12 @@ int rt_last_kernel_ms(rt_ctx* c, double* out_ms) {
   return RT_OK;
 }
 
+int rt_last_launch(rt_ctx* c, rt_launch_info* out) {
+  if (!c || !out) return invalid("null argument");
+  *out = c->last_launch;
+  return RT_OK;
+}
+
 int rt_debug_closest_hits(rt_ctx* c, const double* rays, int n, double tmin, double tmax, uint64_t seed,
                           uint32_t flags, double* out) {
   if (!c || !rays || !out || n < 0) return invalid("null argument");
@@ -1618,7 +1662,7 @@ int rt_debug_closest_hits(rt_ctx* c, const double* rays, int n, double tmin, dou
   if ((flags & RT_DEBUG_WIDE) && !c->d_wnodes)
     return unsupported("rt_debug_closest_hits: no 4-wide tree for this world");
   if (n == 0) return RT_OK;
-  HIPCHK(hipSetDevice(c->device));
+  DEVICE_SCOPE(c->device);
   DevBuf rays_buf, out_buf;
   HIPCHK(hipMalloc(&rays_buf.p, sizeof(double) * 7 * (size_t)n));
   HIPCHK(hipMalloc(&out_buf.p, sizeof(double) * 12 * (size_t)n));
@@ -1642,7 +1686,7 @@ int rt_debug_closest_hits(rt_ctx* c, const double* rays, int n, double tmin, dou
 int rt_debug_math(rt_ctx* c, int op, const double* x, const double* y, int n, double* out) {
   if (!c || !x || !y || !out || n < 0 || op < 0 || op > 11) return invalid("rt_debug_math: bad argument");
   if (n == 0) return RT_OK;
-  HIPCHK(hipSetDevice(c->device));
+  DEVICE_SCOPE(c->device);
   const size_t bytes = sizeof(double) * (size_t)n;
   DevBuf bx, by, bout;
   HIPCHK(hipMalloc(&bx.p, bytes));

@@ -464,4 +464,37 @@ int rt_write_ppm(const uint8_t* rgb, int width, int height, char* buf, size_t ca
   return RT_OK;
 }
 
+// ------------------------------------------------------------------ float dump
+// The per-pixel averages before albedoToColor (rt_render's out_linear), for the per-channel tolerance
+// metric. PFM: "PF\n<W> <H>\n-1.0\n" then little-endian float32 RGB rows from the BOTTOM row up (the
+// format's order). `f64` != 0 writes the same layout with doubles under the header "PF64" (no
+// rounding: the dump parity tests compare). NaN pixels (the reference prints them as 0) stay NaN.
+int rt_write_pfm(const double* linear, int width, int height, int f64, char* buf, size_t cap, size_t* out_len) {
+  if (!linear || width <= 0 || height <= 0) return fail("rt_write_pfm: bad arguments");
+  const std::string head = std::string(f64 ? "PF64" : "PF") + "\n" + std::to_string(width) + " " +
+                           std::to_string(height) + "\n-1.0\n";
+  const size_t px = (size_t)width * height * 3, elem = f64 ? sizeof(double) : sizeof(float);
+  const size_t n = head.size() + px * elem;
+  if (out_len) *out_len = n;
+  if (!buf || !cap) return RT_OK;
+  std::string s;
+  s.reserve(n);
+  s += head;
+  for (int row = height - 1; row >= 0; --row) {
+    const double* src = linear + (size_t)row * width * 3;
+    for (int i = 0; i < width * 3; ++i) {
+      unsigned char b[8];
+      if (f64) {
+        std::memcpy(b, &src[i], 8);
+      } else {
+        const float f = (float)src[i];
+        std::memcpy(b, &f, 4);
+      }
+      s.append((const char*)b, elem);  // (x86-64 / gfx950 hosts are little-endian)
+    }
+  }
+  std::memcpy(buf, s.data(), std::min(cap, s.size()));
+  return RT_OK;
+}
+
 }  // extern "C"

@@ -561,6 +561,8 @@ struct Trav {
   int best_level;     // F_INST: frames around the best hit (copied to Side::best)
   bool tie;           // a second leaf hit at exactly `closest`: the walk is redone with `ref`
   bool ref;           // the reference's own walk: caller's tree, left first, bound = closest
+  bool redo;          // a tie redo: reference semantics on every node (no RT_SUB subtrees, left
+                      // child first even under RT_BVH_ORDERED nodes), so it never flags a tie
   // F_WIDE: the ray in fp32 for the conservative child-box test (wide_keys2)
   float o32x, o32y, o32z, i32x, i32y, i32z;
   float slack, tmin32, tmax32;  // slack = +inf: the fp32 distances say nothing, accept every child
@@ -591,6 +593,7 @@ __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r, int root, doub
   t.best_level = 0;
   t.tie = false;
   t.ref = false;
+  t.redo = false;
   if constexpr ((F & F_WIDE) != 0) {
     t.node = 0;  // wide root
     t.o32x = (float)r.o.x;
@@ -624,9 +627,12 @@ __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r, int root, doub
   }
 }
 
-// Redo the walk as the reference does it: the caller's tree, left child first (its nodes carry
-// no RT_BVH_ORDERED), every accepted hit replacing the best under bound = closest.
-__device__ __forceinline__ void trav_restart_ref(Trav& t, int root, double t_max) {
+// Redo the walk as the reference does it: the caller's tree, left child first, every accepted hit
+// replacing the best under bound = closest. `redo` (a walk redone for an exact tie) applies those
+// semantics to every node: a caller's tree may itself hold RT_BVH_ORDERED nodes (rt_rebuild_bvh
+// output uploaded again), which in the first walk of a mixed world mark re-bounded subtrees whose
+// leaves flag ties — in a redo that would flag the same tie again, forever.
+__device__ __forceinline__ void trav_restart_ref(Trav& t, int root, double t_max, bool redo = false) {
   t.node = root;
   t.sp = 0;
   t.closest = t_max;
@@ -639,6 +645,7 @@ __device__ __forceinline__ void trav_restart_ref(Trav& t, int root, double t_max
   t.best_level = 0;
   t.tie = false;
   t.ref = true;
+  t.redo = redo;
 }
 
 // Leaf of the resumable walk (a primitive, or an instance chain ending in one). Leaves are tested
@@ -802,7 +809,7 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
     if constexpr ((F & F_COUNT) != 0) ++cnt.box;
     if (box_hit(n->f, t.ray, t_min, refsem ? t.closest : t.closest_up, joint)) {
       const int c = n->c;
-      const bool ord = (c & RT_BVH_ORDERED) != 0;
+      const bool ord = (c & RT_BVH_ORDERED) && !t.redo;
       const bool flip = ord && comp(t.ray.d, c & 3) < 0;
       const int ctag = (kRefMixed<F> && ord) ? RT_SUB : tag;
       stk[(t.sp++) * stride] = (flip ? n->a : n->b) | ctag;

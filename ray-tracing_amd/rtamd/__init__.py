@@ -31,6 +31,7 @@ RT_NODE_CONSTANT_MEDIUM, RT_NODE_UNHITTABLE, RT_NODE_EXT = 9, 10, 11
 RT_RNG_EXACT, RT_RNG_PHILOX = 0, 1
 RT_FLAG_NAN_CULL = 1
 RT_FLAG_REFERENCE_CULL = 2
+RT_FLAG_NAN_ZERO = 4  # parity diagnostic: NaN sample channels add 0 (rt.h)
 RT_UPLOAD_REFERENCE_BVH = 1
 RT_DEBUG_RESUMABLE = 4  # rt_debug_closest_hits: the render loop's resumable binary walk
 RT_DEBUG_WIDE = 8       # rt_debug_closest_hits: the resumable walk over the 4-wide fp32-box tree
@@ -87,6 +88,12 @@ class rt_camera(C.Structure):
         ("lens_radius", C.c_double), ("t0", C.c_double), ("t1", C.c_double)]
 
 
+class rt_launch_info(C.Structure):
+    _fields_ = [("variant", C.c_uint32), ("loop", C.c_int32), ("lds_staged", C.c_int32), ("leaf_lds", C.c_int32),
+                ("waves", C.c_int32), ("grid", C.c_int32), ("block", C.c_int32), ("dyn_lds_bytes", C.c_int32),
+                ("work_items", C.c_int64), ("chunk", C.c_int32), ("_pad", C.c_int32)]
+
+
 class rt_render_params(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_int32), ("max_depth", C.c_int32),
                 ("rng_mode", C.c_int32), ("flags", C.c_uint32), ("seed", C.c_uint64), ("tile", C.c_int32),
@@ -108,7 +115,7 @@ EXPORTED = [
     "rt_device_count", "rt_create", "rt_destroy", "rt_upload_scene", "rt_render", "rt_shard_geometry",
     "rt_render_shard_async", "rt_assemble_async", "rt_assemble_linear_async", "rt_last_kernel_ms",
     "rt_debug_closest_hits", "rt_debug_math", "rt_render_work", "rt_upload_scene_ex", "rt_rebuild_bvh",
-    "rt_wide_bvh", "rt_tree_stack_need",
+    "rt_wide_bvh", "rt_tree_stack_need", "rt_last_launch", "rt_write_pfm",
 ]
 
 # include/rt_wide.h: one 4-wide node (128 B)
@@ -184,6 +191,8 @@ def lib() -> C.CDLL:
             "rt_rebuild_bvh": (I, [P(rt_scene_desc), P(rt_node), I, P(I), P(I)]),
             "rt_wide_bvh": (I, [P(rt_node), I, I, C.c_void_p, I, P(I), P(I)]),
             "rt_tree_stack_need": (I, [P(rt_node), I, I, P(I)]),
+            "rt_last_launch": (I, [C.c_void_p, P(rt_launch_info)]),
+            "rt_write_pfm": (I, [P(D), I, I, I, C.c_char_p, C.c_size_t, P(C.c_size_t)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -520,6 +529,13 @@ class Context:
         out["tie_redos"] = int(w[15])  # replacement loop only: walks (or samples) redone for an exact tie
         return out
 
+    def last_launch(self) -> dict:
+        """rt_last_launch: which kernel the last tier-B render launch ran (variant bits, loop, LDS
+        staging, waves per SIMD, grid, block, dynamic LDS, work-items, samples per work-item)."""
+        info = rt_launch_info()
+        _check(lib().rt_last_launch(self._h, C.byref(info)), "rt_last_launch")
+        return {k: getattr(info, k) for k, _ in rt_launch_info._fields_ if k != "_pad"}
+
     def last_kernel_ms(self) -> float:
         ms = C.c_double(0)
         _check(lib().rt_last_kernel_ms(self._h, C.byref(ms)), "rt_last_kernel_ms")
@@ -588,6 +604,29 @@ def write_ppm(rgb: np.ndarray) -> bytes:
     buf = C.create_string_buffer(n.value)
     _check(lib().rt_write_ppm(rgb.ctypes.data_as(P(C.c_uint8)), W, H, buf, n.value, C.byref(n)), "rt_write_ppm")
     return buf.raw[: n.value]
+
+
+def write_pfm(linear: np.ndarray, f64: bool = False) -> bytes:
+    """rt_write_pfm: the per-pixel averages (H x W x 3 doubles, top row first) as PFM (float32, bottom
+    row first) or, with f64, the lossless "PF64" variant."""
+    lin = np.ascontiguousarray(linear, dtype=np.float64)
+    H, W, _ = lin.shape
+    n = C.c_size_t(0)
+    P = C.POINTER
+    _check(lib().rt_write_pfm(lin.ctypes.data_as(P(C.c_double)), W, H, int(f64), None, 0, C.byref(n)), "rt_write_pfm")
+    buf = C.create_string_buffer(n.value)
+    _check(lib().rt_write_pfm(lin.ctypes.data_as(P(C.c_double)), W, H, int(f64), buf, n.value, C.byref(n)),
+           "rt_write_pfm")
+    return buf.raw[: n.value]
+
+
+def read_pfm(data: bytes) -> np.ndarray:
+    """Parse rt_write_pfm output back to H x W x 3 float64, top row first."""
+    magic, dims, scale, rest = data.split(b"\n", 3)
+    W, H = (int(x) for x in dims.split())
+    dt = "<f8" if magic == b"PF64" else ("<f4" if float(scale) < 0 else ">f4")
+    a = np.frombuffer(rest, dtype=dt, count=W * H * 3).astype(np.float64).reshape(H, W, 3)
+    return a[::-1].copy()
 
 
 # ----------------------------------------------------------------------------- tiling (host mirror)

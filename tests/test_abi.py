@@ -82,3 +82,17 @@ def test_render_without_device_fails_loudly():
         pytest.skip("GPU present")
     with pytest.raises(rtamd.RTError):
         rtamd.Context(0)
+
+
+def test_pfm_float_dump_round_trip():
+    """rt_write_pfm: PFM float32 bottom row first, and the lossless PF64 variant;
+    NaN pixels stay NaN."""
+    lin = np.random.default_rng(1).random((5, 7, 3))
+    lin[2, 3] = np.nan
+    pf = rtamd.write_pfm(lin)
+    assert pf.startswith(b"PF\n7 5\n-1.0\n") and len(pf) == len(b"PF\n7 5\n-1.0\n") + 5 * 7 * 3 * 4
+    first = np.frombuffer(pf[len(b"PF\n7 5\n-1.0\n"):][:7 * 3 * 4], dtype="<f4")
+    assert np.array_equal(first, lin[4].reshape(-1).astype(np.float32))  # bottom row first
+    back = rtamd.read_pfm(pf)
+    assert np.array_equal(back, lin.astype(np.float32).astype(np.float64), equal_nan=True)
+    assert np.array_equal(rtamd.read_pfm(rtamd.write_pfm(lin, f64=True)), lin, equal_nan=True)

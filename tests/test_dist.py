@@ -53,3 +53,56 @@ def test_gloo_two_ranks_gather():
         p.join(120)
     assert all(p.exitcode == 0 for p in procs)
     assert q.get(timeout=5) is True
+
+
+def _frame_worker(rank, world, port, W, H, tile, q):
+    """bench.py's step through rtamd.frame.ShardedFrame on the CPU: the renderer fills the rank's
+    slab from a reference image through the shard map (as rt_render_shard_async lays it out), the
+    slabs are all-gathered over gloo, rank 0 assembles with the assemble kernel's host restatement."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "ray-tracing_amd"))
+    import torch
+    import torch.distributed as dist
+    import rtamd
+    from rtamd.frame import ShardedFrame, host_assembler
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    img = np.random.default_rng(7).integers(0, 256, (H, W, 3), dtype=np.uint8)
+    p = rtamd.make_params(W, H, 1, 1, tile=tile, shard_rank=rank, shard_count=world)
+    calls = []
+
+    def render(params, slab):
+        m = rtamd.shard_pixel_map(params)
+        s = np.zeros((m.size, 3), dtype=np.uint8)
+        s[m >= 0] = img.reshape(-1, 3)[m[m >= 0]]
+        slab.copy_(torch.from_numpy(s))
+        calls.append(params.shard_rank)
+
+    f = ShardedFrame(p, world, rank, "cpu", backend="gloo", render=render, assemble=host_assembler())
+    for _ in range(2):
+        f.step()
+    t = f.finish()
+    ok = len(t) == 2 and calls == [rank, rank]
+    if rank == 0:
+        ok = ok and bool(np.array_equal(f.image.numpy(), img))
+    q.put((rank, ok))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_sharded_frame_steps():
+    """World size 3 (tiles dealt unevenly: 8 x 5 tiles over 3 ranks, padded slabs), two steps."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 3
+    procs = [ctx.Process(target=_frame_worker, args=(r, world, port, 120, 72, 16, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    res = dict(q.get(timeout=5) for _ in range(world))
+    assert all(res.values()), res

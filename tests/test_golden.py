@@ -75,6 +75,7 @@ def test_oracle_closest_hits_golden(name):
 def _check_image(rgb, lin, key):
     lin_g = G[f"{key}_lin"]
     ok, eq, dmax = parity(lin[: lin_g.shape[0]], lin_g, rgb, G[f"{key}_rgb"])
+    print(f"{key}: channels within 1e-3 {ok:.6f}, bytes equal {eq:.6f}, max |d| {dmax:.3g}")
     assert ok >= 0.999, f"{key}: {ok:.5f} of channels within 1e-3 (max |d| {dmax:.3g})"
     assert eq >= 0.999, f"{key}: {eq:.5f} of bytes equal"
 
@@ -94,7 +95,8 @@ def test_gpu_config1_tier_a_golden(gpu_ctx):
     rgb, lin, go = gpu_ctx.render(cam, rtamd.make_params(200, 100, 10, 10, rtamd.RT_RNG_EXACT),
                                   G["c1a_gens_in"], linear=True, want_gens=True)
     _check_image(rgb, lin, "c1a")
-    assert (go == G["c1a_gens_out"]).all(axis=1).mean() >= 0.99
+    print(f"c1a: end generators equal in {(go == G['c1a_gens_out']).all(axis=1).mean():.6f} of columns")
+    assert np.array_equal(go, G["c1a_gens_out"])
 
 
 @pytest.mark.gpu
@@ -104,7 +106,8 @@ def test_gpu_cornell_tier_a_golden(gpu_ctx):
     rgb, lin, go = gpu_ctx.render(cam, rtamd.make_params(64, 64, 16, 50, rtamd.RT_RNG_EXACT),
                                   G["cba_gens_in"], linear=True, want_gens=True)
     _check_image(rgb, lin, "cba")
-    assert (go == G["cba_gens_out"]).all(axis=1).mean() >= 0.99
+    print(f"cba: end generators equal in {(go == G['cba_gens_out']).all(axis=1).mean():.6f} of columns")
+    assert np.array_equal(go, G["cba_gens_out"])
 
 
 @pytest.mark.gpu

@@ -18,6 +18,8 @@ def _cmp(ctx, scene, cam, p, col_gens=None):
     rgb_g, lin_g, gens_g = ctx.render(cam, p, col_gens, linear=True, want_gens=col_gens is not None)
     rgb_o, lin_o, gens_o, _ = pyoracle.render(scene, cam, p, col_gens=col_gens)
     ok, eq, dmax = parity(lin_g, lin_o, rgb_g, rgb_o)
+    print(f"{p.width}x{p.height}x{p.spp} d{p.max_depth}: channels within 1e-3 {ok:.6f}, bytes equal {eq:.6f}, "
+          f"max |d| {dmax:.3g}")
     assert ok >= 0.999 and eq >= 0.999, (ok, eq, dmax)
     if col_gens is not None:
         assert np.array_equal(gens_g, gens_o)

@@ -51,7 +51,8 @@ def test_nested_frames(gpu_ctx, depth, medium, monkeypatch):
     rgb, lin, _ = gpu_ctx.render(cam, p, linear=True)
     rgb_o, lin_o, _, _ = pyoracle.render(sc, cam, p)
     ok, eq, dmax = parity(lin, lin_o, rgb, rgb_o)
-    assert ok >= 0.995 and eq >= 0.995, (ok, eq, dmax)
+    print(f"frames depth {depth} medium {medium}: channels within 1e-3 {ok:.6f}, bytes equal {eq:.6f}, max |d| {dmax:.3g}")
+    assert ok >= 0.999 and eq >= 0.999, (ok, eq, dmax)
     monkeypatch.setenv("RTAMD_REPLACE", "0")
     rgb_s, lin_s, _ = gpu_ctx.render(cam, p, linear=True)
     assert np.array_equal(rgb, rgb_s) and np.array_equal(lin, lin_s, equal_nan=True)
@@ -143,3 +144,27 @@ def test_launches_on_two_streams_are_ordered(gpu_ctx):
     torch.cuda.synchronize()
     for b, r in zip(bufs, ref):
         assert np.array_equal(b.cpu().numpy(), r)
+
+
+@pytest.mark.parametrize("name,camname", [("next_week_final", "next_week"), ("random", "random_scene")])
+def test_rebuilt_world_uploaded_again(gpu_ctx, name, camname):
+    """A caller's world tree that already holds RT_BVH_ORDERED nodes (rt_rebuild_bvh output, e.g.
+    rtamd.rebuilt_scene, uploaded again): media and textured worlds render to the oracle's image of
+    the original scene (next_week_final: media, frames, Perlin and image textures; random: moving
+    spheres, checker and image textures), and walks redone for an exact tie treat every node with the reference's
+    semantics (before, such a redo could flag the same tie forever)."""
+    earth = np.load(os.path.join(os.path.dirname(__file__), "golden", "earthmap_rgb8.npz"))["rgb"]
+    sc, _ = rtamd.make_scene(name, rtamd.randGen(1024), earth=earth)
+    rb = rtamd.rebuilt_scene(sc)
+    assert (rb.nodes["c"] & rtamd.RT_BVH_ORDERED).any()
+    cam = rtamd.camera(camname, 48, 40)
+    p = rtamd.make_params(48, 40, 4, 50, rtamd.RT_RNG_PHILOX, seed=13)
+    gpu_ctx.upload(rb)
+    rgb, lin, _ = gpu_ctx.render(cam, p, linear=True)
+    w = gpu_ctx.render_work(cam, p)
+    rgb_o, lin_o, _, _ = pyoracle.render(sc, cam, p)
+    ok, eq, dmax = parity(lin, lin_o, rgb, rgb_o)
+    print(f"{name} rebuilt + re-uploaded: channels within 1e-3 {ok:.6f}, bytes equal {eq:.6f}, max |d| {dmax:.3g}, "
+          f"tie redos {w['tie_redos']}")
+    assert w["samples"] == 48 * 40 * 4
+    assert ok >= 0.999 and eq >= 0.999, (ok, eq, dmax)
