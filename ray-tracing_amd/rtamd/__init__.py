@@ -568,20 +568,28 @@ def shard_geometry(params: rt_render_params) -> Tuple[int, int, int]:
 
 def runRender(env: RenderStaticEnv, gens: Sequence[Tuple[int, int]], device: int = 0,
               ctx: Optional[Context] = None) -> List[np.ndarray]:
-    """runRender (src/Lib.hs:1491): tier A, one generator per column; rows top first."""
+    """runRender (src/Lib.hs:1491): tier A, generator x for column x; rows top first.
+
+    As the reference's `VV.zip gs row` (src/Lib.hs:1519), every row holds min(len(gens), W) pixels:
+    extra generators are ignored, and with fewer generators than columns the rows are truncated to
+    the first len(gens) columns (a column's stream depends only on its own generator and position,
+    so the missing columns are rendered with copies of the first generator and cut off)."""
     W, H = env.size
-    if len(gens) != W:
-        raise RTError("runRender needs exactly one generator per image column")
+    gens = list(gens)[:W]
+    cols = len(gens)
+    if cols == 0 or H <= 0:
+        return [np.zeros((0, 3), dtype=np.uint8) for _ in range(max(0, H))]
+    full = gens + [gens[0]] * (W - cols)
     own = ctx is None
     ctx = ctx or Context(device)
     try:
         ctx.upload(env.scene)
         p = make_params(W, H, env.num_samples, env.max_depth, RT_RNG_EXACT)
-        rgb, _, _ = ctx.render(env.camera, p, np.array(gens, dtype=np.uint64))
+        rgb, _, _ = ctx.render(env.camera, p, np.array(full, dtype=np.uint64))
     finally:
         if own:
             ctx.close()
-    return [rgb[i] for i in range(H)]
+    return [rgb[i, :cols].copy() for i in range(H)]
 
 
 def column_gens(g1: Tuple[int, int], width: int, seed: int = 1024) -> np.ndarray:

@@ -1,0 +1,223 @@
+/*
+ * ffi_sequence.c — the call sequence of integration/RenderAMD.hs (the Haskell FFI module, which
+ * cannot be compiled here: no GHC), run in C through include/rt.h.
+ *
+ * RenderAMD.flattenScene walks the reference's Hittable tree (src/Lib.hs:521-585) in post-order and
+ * emits one record per occurrence: shared values (the Cornell light in both trees, BVHNode h h, a
+ * medium's boundary) are duplicated, every leaf gets its own material copy, every material its own
+ * texture copy (checker children first), every Perlin / image texture its own table / raster. This
+ * program re-flattens a builder-made scene (rt_scene_named: the restated Scenes.hs builders) the same
+ * way from its roots, then:
+ *   CPU: checks the re-flattened descriptor is well formed for the library (rt_rebuild_bvh,
+ *        rt_tree_stack_need) and that the duplication is what the Haskell module produces;
+ *   GPU (argv[1] == "gpu"): runs runRenderAMD's sequence — rt_create, rt_upload_scene, rt_render in
+ *        tier A with one (seed, gamma) per column (the deterministic app/Main.hs:47-49 harness:
+ *        column 0 = the builder's g1, column x = randGen (1024 + x)), rt_destroy — and checks the bytes
+ *        and end-of-stream generators equal those of the builder's own descriptor; tier B too.
+ * Exit 0 on success; prints one line per scene.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "rt.h"
+
+typedef struct {
+  rt_node* nodes; int n, cap;
+  rt_material* mats; int nm, capm;
+  rt_texture* texs; int nt, capt;
+  rt_perlin* perlins; int np, capp;
+  rt_image* images; int ni, capi;
+  uint8_t* pool; int64_t pool_bytes, cap_pool;
+} Flat;
+
+#define PUSH(arr, n, cap, x)                                          \
+  do {                                                                \
+    if ((n) == (cap)) {                                               \
+      (cap) = (cap) ? 2 * (cap) : 64;                                 \
+      (arr) = realloc((arr), sizeof(*(arr)) * (size_t)(cap));         \
+    }                                                                 \
+    (arr)[(n)++] = (x);                                               \
+  } while (0)
+
+static const rt_scene_desc* S; /* the builder's descriptor being re-flattened */
+
+/* textureValue's tree (src/Lib.hs:394-419) -> one copy per occurrence, children first */
+static int flat_tex(Flat* f, int tid) {
+  rt_texture t = S->textures[tid];
+  if (t.type == RT_TEX_CHECKER) {
+    t.a = flat_tex(f, t.a);
+    t.b = flat_tex(f, t.b);
+  } else if (t.type == RT_TEX_PERLIN) {
+    PUSH(f->perlins, f->np, f->capp, S->perlins[t.a]);
+    t.a = f->np - 1;
+  } else if (t.type == RT_TEX_IMAGE && t.a >= 0) {
+    const rt_image im = S->images[t.a];
+    const int64_t bytes = (int64_t)im.width * im.height * 3;
+    if (f->pool_bytes + bytes > f->cap_pool) {
+      f->cap_pool = 2 * (f->pool_bytes + bytes);
+      f->pool = realloc(f->pool, (size_t)f->cap_pool);
+    }
+    memcpy(f->pool + f->pool_bytes, S->image_pool + im.offset, (size_t)bytes);
+    rt_image ni = {f->pool_bytes, im.width, im.height};
+    f->pool_bytes += bytes;
+    PUSH(f->images, f->ni, f->capi, ni);
+    t.a = f->ni - 1;
+  }
+  PUSH(f->texs, f->nt, f->capt, t);
+  return f->nt - 1;
+}
+
+static int flat_mat(Flat* f, int mid) {
+  rt_material m = S->materials[mid];
+  if (m.type != RT_MAT_DIELECTRIC) m.texture = flat_tex(f, m.texture);
+  else m.texture = -1; /* (Dielectric has no texture: RenderAMD emits -1) */
+  PUSH(f->mats, f->nm, f->capm, m);
+  return f->nm - 1;
+}
+
+/* the Hittable tree, post-order (RenderAMD.flatHit) */
+static int flat_hit(Flat* f, int id) {
+  rt_node x = S->nodes[id];
+  switch (x.type) {
+    case RT_NODE_BVH: {
+      const int a = flat_hit(f, x.a), b = flat_hit(f, x.b);
+      x.a = a;
+      x.b = b;
+      break;
+    }
+    case RT_NODE_SPHERE:
+    case RT_NODE_RECT_XY:
+    case RT_NODE_RECT_XZ:
+    case RT_NODE_RECT_YZ:
+    case RT_NODE_CUBOID:
+      x.a = flat_mat(f, x.a);
+      break;
+    case RT_NODE_MOVING_SPHERE: {
+      x.a = flat_mat(f, x.a);
+      PUSH(f->nodes, f->n, f->cap, x);
+      PUSH(f->nodes, f->n, f->cap, S->nodes[id + 1]); /* its EXT record right after */
+      return f->n - 2;
+    }
+    case RT_NODE_TRANSLATE:
+    case RT_NODE_ROTATE:
+      x.a = flat_hit(f, x.a);
+      break;
+    case RT_NODE_CONSTANT_MEDIUM: {
+      const int b = flat_hit(f, x.a);
+      x.a = b;
+      x.b = flat_mat(f, x.b);
+      break;
+    }
+    default:
+      break; /* Unhittable */
+  }
+  PUSH(f->nodes, f->n, f->cap, x);
+  return f->n - 1;
+}
+
+static int fail(const char* what) {
+  fprintf(stderr, "FAIL %s: %s\n", what, rt_last_error());
+  return 1;
+}
+
+static int run(int scene_id, const char* name, int cam_id, int W, int H, int spp, int gpu) {
+  uint64_t g[2];
+  rt_rand_gen(1024, g);
+  rt_builder* b;
+  if (rt_builder_create(g, &b)) return fail("rt_builder_create");
+  /* a synthetic 64x32 earth raster (the real one is a fixture the C test does not parse) */
+  uint8_t earth[64 * 32 * 3];
+  for (int i = 0; i < 64 * 32 * 3; ++i) earth[i] = (uint8_t)(i * 37 + 11);
+  rt_scene_desc a;
+  if (rt_scene_named(b, scene_id, 0.0, 1.0, earth, 64, 32, 0, &a)) return fail("rt_scene_named");
+  uint64_t g1[2];
+  rt_builder_gen(b, g1);
+
+  /* RenderAMD.flattenScene */
+  S = &a;
+  Flat f;
+  memset(&f, 0, sizeof f);
+  const int world = flat_hit(&f, a.world_root);
+  const int lights = a.lights_root < 0 ? -1 : flat_hit(&f, a.lights_root);
+  rt_scene_desc d = a;
+  d.nodes = f.nodes;
+  d.n_nodes = f.n;
+  d.world_root = world;
+  d.lights_root = lights;
+  d.materials = f.mats;
+  d.n_materials = f.nm;
+  d.textures = f.texs;
+  d.n_textures = f.nt;
+  d.perlins = f.perlins;
+  d.n_perlins = f.np;
+  d.images = f.images;
+  d.n_images = f.ni;
+  d.image_pool = f.pool;
+  d.image_pool_bytes = f.pool_bytes;
+
+  /* CPU: well formed for the library, same stack bound, duplication as the Haskell module's */
+  int n1 = 0, r1 = 0, need_a = 0, need_d = 0;
+  if (rt_rebuild_bvh(&d, NULL, 0, &n1, &r1)) return fail("rt_rebuild_bvh(flattened)");
+  if (rt_tree_stack_need(a.nodes, a.n_nodes, a.world_root, &need_a) ||
+      rt_tree_stack_need(d.nodes, d.n_nodes, d.world_root, &need_d))
+    return fail("rt_tree_stack_need");
+  if (need_a != need_d) {
+    fprintf(stderr, "FAIL %s: stack need %d vs %d\n", name, need_a, need_d);
+    return 1;
+  }
+  if (d.n_nodes < a.n_nodes - 1 || d.n_materials < 1) {
+    fprintf(stderr, "FAIL %s: flattened %d nodes from %d\n", name, d.n_nodes, a.n_nodes);
+    return 1;
+  }
+  printf("%s: builder %d nodes / %d materials / %d textures -> flattened %d / %d / %d, stack need %d",
+         name, a.n_nodes, a.n_materials, a.n_textures, d.n_nodes, d.n_materials, d.n_textures, need_d);
+
+  int rc = 0;
+  if (gpu) {
+    rt_camera cam;
+    if (rt_camera_named(cam_id, W, H, &cam)) return fail("rt_camera_named");
+    uint64_t* gens = malloc(sizeof(uint64_t) * 2 * (size_t)W);
+    gens[0] = g1[0];
+    gens[1] = g1[1];
+    for (int x = 1; x < W; ++x) rt_rand_gen(1024 + x, gens + 2 * x);
+    uint8_t *rgb_a = malloc((size_t)W * H * 3), *rgb_d = malloc((size_t)W * H * 3);
+    uint64_t *go_a = malloc(sizeof(uint64_t) * 2 * (size_t)W), *go_d = malloc(sizeof(uint64_t) * 2 * (size_t)W);
+    for (int tier = 0; tier < 2 && !rc; ++tier) {
+      rt_render_params p = {W, H, spp, 50, tier ? RT_RNG_PHILOX : RT_RNG_EXACT, 0, 1024, 16, 0, 1, 0};
+      for (int which = 0; which < 2 && !rc; ++which) {
+        rt_ctx* ctx; /* runRenderAMD: rt_create, rt_upload_scene, rt_render, rt_destroy */
+        if (rt_create(0, &ctx)) return fail("rt_create");
+        if (rt_upload_scene(ctx, which ? &d : &a)) rc = fail("rt_upload_scene");
+        else if (rt_render(ctx, &cam, &p, gens, which ? rgb_d : rgb_a, NULL, which ? go_d : go_a))
+          rc = fail("rt_render");
+        rt_destroy(ctx);
+      }
+      if (!rc && memcmp(rgb_a, rgb_d, (size_t)W * H * 3)) {
+        fprintf(stderr, "FAIL %s: tier %c bytes differ\n", name, tier ? 'B' : 'A');
+        rc = 1;
+      }
+      if (!rc && !tier && memcmp(go_a, go_d, sizeof(uint64_t) * 2 * (size_t)W)) {
+        fprintf(stderr, "FAIL %s: tier A end generators differ\n", name);
+        rc = 1;
+      }
+    }
+    if (!rc) printf(", GPU tier A + B %dx%dx%d: identical bytes and end generators", W, H, spp);
+    free(gens), free(rgb_a), free(rgb_d), free(go_a), free(go_d);
+  }
+  printf("\n");
+  free(f.nodes), free(f.mats), free(f.texs), free(f.perlins), free(f.images), free(f.pool);
+  rt_builder_destroy(b);
+  return rc;
+}
+
+int main(int argc, char** argv) {
+  const int gpu = argc > 1 && !strcmp(argv[1], "gpu");
+  int rc = 0;
+  rc |= run(RT_SCENE_CORNELL_BOX, "cornell", RT_CAM_CORNELL, 40, 40, 4, gpu);
+  rc |= run(RT_SCENE_NEXT_WEEK_FINAL, "next_week_final", RT_CAM_NEXT_WEEK, 32, 24, 2, gpu);
+  rc |= run(RT_SCENE_RANDOM, "random", RT_CAM_RANDOM_SCENE, 40, 24, 2, gpu);
+  rc |= run(RT_SCENE_CORNELL_SMOKE, "cornell_smoke", RT_CAM_CORNELL, 32, 32, 2, gpu);
+  return rc;
+}

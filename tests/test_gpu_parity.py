@@ -345,3 +345,20 @@ def test_work_claims_do_not_change_the_image(gpu_ctx, name, cam, monkeypatch):
         assert gpu_ctx.render_work(c, p)["samples"] == 128 * 96 * 24
     for rgb, lin, _ in out[1:]:
         assert np.array_equal(rgb, out[0][0]) and np.array_equal(lin, out[0][1], equal_nan=True)
+
+
+def test_run_render_zip_truncation(gpu_ctx):
+    """runRender zips the generators with each row (src/Lib.hs:1519): fewer generators than
+    columns truncate every row to that many pixels (the same bytes as those columns of the full
+    render), extra generators are ignored, none gives empty rows."""
+    sc, g1 = _scene("three_spheres")
+    cam = rtamd.camera("random_scene", 48, 24)
+    env = rtamd.mkRenderStaticEnv(sc, cam, (48, 24), 3, 10)
+    gens = [tuple(int(v) for v in g) for g in rtamd.column_gens(g1, 60)]
+    full = rtamd.runRender(env, gens[:48], ctx=gpu_ctx)
+    assert len(full) == 24 and all(r.shape == (48, 3) for r in full)
+    short = rtamd.runRender(env, gens[:41], ctx=gpu_ctx)
+    assert all(r.shape == (41, 3) for r in short)
+    assert all(np.array_equal(a, b[:41]) for a, b in zip(short, full))
+    assert all(np.array_equal(a, b) for a, b in zip(rtamd.runRender(env, gens, ctx=gpu_ctx), full))
+    assert all(r.shape == (0, 3) for r in rtamd.runRender(env, [], ctx=gpu_ctx))
