@@ -538,6 +538,10 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
       // worlds with media or frames: the reference's order over the re-bounded skeleton
       if (S.ref_walk) trav_restart_ref(t, S.world, INFINITY);
       if constexpr (kRefMixed<F>) walk_mark = g.consumed();
+      // (media draw inside the walk: top the FIFO up here, where the starting lanes run together,
+      // so that a medium's draw does not evaluate Philox inside a divergent walk step; the words and
+      // their order are the stream's, and consumed() is unchanged)
+      if constexpr ((F & F_MEDIA) != 0) g.reserve(2);
       walking = true;
     }
     if (!walking) break;  // this lane is finished; the rest of the wave carries on without it

@@ -373,14 +373,29 @@ __device__ inline bool chain_t(const Scene& S, int id, const Ray& ray, double t_
   return prim_t<F>(S, &S.nodes[cur], prep(r), t_min, t_max, t, sub);
 }
 
+// chain_t for a ray whose reciprocals are already known (the walk's RayX): a boundary that is a plain
+// primitive is tested with them directly — prep() of the same ray gives the same values, so only
+// the recomputation is saved (4 fp64 divisions per query); an instance chain transforms the ray.
+template <unsigned F>
+__device__ __forceinline__ bool chain_tx(const Scene& S, int id, const RayX& rx, double t_min, double t_max,
+                                         double& t) {
+  if constexpr ((F & F_INST) != 0) {
+    const int type = S.nodes[id].type & RT_TYPE_MASK;
+    if (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE) return chain_t<F>(S, id, plain(rx), t_min, t_max, t);
+  }
+  int sub;
+  return prim_t<F>(S, &S.nodes[id], rx, t_min, t_max, t, sub);
+}
+
 // hit ConstantMedium (Lib.hs:1053-1080). The boundary is a primitive chain (host-validated); only
 // the two boundary hits' t are used.
 template <unsigned F, class R>
-__device__ inline bool medium_hit(const Scene& S, const rt_node* n, const Ray& r, double t_min, double t_max, R& g,
+__device__ inline bool medium_hit(const Scene& S, const rt_node* n, const RayX& rx, double t_min, double t_max, R& g,
                                   Hit& h) {
+  const Ray r = plain(rx);
   double t1, t2;
-  if (!chain_t<F>(S, n->a, r, -INFINITY, INFINITY, t1)) return false;
-  if (!chain_t<F>(S, n->a, r, t1 + kEps, INFINITY, t2)) return false;
+  if (!chain_tx<F>(S, n->a, rx, -INFINITY, INFINITY, t1)) return false;
+  if (!chain_tx<F>(S, n->a, rx, t1 + kEps, INFINITY, t2)) return false;
   const double rec1tp = gmax(t_min, t1);
   const double rec2t = gmin(t_max, t2);
   if (rec1tp >= rec2t) return false;
@@ -457,7 +472,7 @@ __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr
     } else if ((F & F_MEDIA) && type == RT_NODE_CONSTANT_MEDIUM) {
       if constexpr ((F & F_COUNT) != 0) ++cnt.other;
       Hit h;
-      if (medium_hit<F>(S, n, plain(ray), t_min, closest, g, h)) {
+      if (medium_hit<F>(S, n, ray, t_min, closest, g, h)) {
         best = h;
         closest = h.t;
         best_node = node;
@@ -691,7 +706,7 @@ __device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, const rt_node
   } else if ((F & F_MEDIA) && type == RT_NODE_CONSTANT_MEDIUM) {  // (always on the skeleton: refsem)
     if constexpr ((F & F_COUNT) != 0) ++cnt.other;
     Hit h;
-    if (medium_hit<F>(S, n, plain(t.ray), t_min, t.closest, g, h)) trav_take<F>(t, h.t, id, kSubMedium, side, true);
+    if (medium_hit<F>(S, n, t.ray, t_min, t.closest, g, h)) trav_take<F>(t, h.t, id, kSubMedium, side, true);
   } else {
     if constexpr ((F & F_COUNT) != 0) ++cnt.prim;
     double tt;
