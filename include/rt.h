@@ -420,6 +420,26 @@ int rt_debug_closest_hits(rt_ctx* ctx, const double* rays, int n, double tmin, d
                           uint64_t seed, uint32_t flags, double* out);
 
 /*
+ * Debug / parity entry: single hot-path functions on the device (golden vectors per function,
+ * tests/golden/make_function_goldens.py). Record i draws from its own tier-B Philox stream
+ * (key = seed, pid = i, sample 0). Layouts (doubles per record), in -> out:
+ *   RT_PROBE_SCATTER      scatter (src/Lib.hs:822-865; emitted 880-885 for DiffuseLight):
+ *                         ray o3 d3 tm, hit t p3 n3 u v front_face material (18) ->
+ *                         scattered (0/1), ray o3 d3 tm, att3 (the emission when not scattered),
+ *                         pdf, specular, Philox words consumed (14)
+ *   RT_PROBE_HTBL_RANDOM  htblRandom on the lights tree (src/Lib.hs:707-724): origin3 -> dir3, words
+ *   RT_PROBE_HTBL_PDF     htblPdfValue on the lights tree (src/Lib.hs:673-705): origin3, v3 -> pdf, words
+ *   RT_PROBE_TEXTURE      textureValue (src/Lib.hs:496-513): texture id, u, v, p3 -> albedo3
+ *   RT_PROBE_GET_RAY      getRay with `cam` (src/Lib.hs:1253-1267): s, t -> ray o3 d3 tm, words
+ */
+#define RT_PROBE_SCATTER 0
+#define RT_PROBE_HTBL_RANDOM 1
+#define RT_PROBE_HTBL_PDF 2
+#define RT_PROBE_TEXTURE 3
+#define RT_PROBE_GET_RAY 4
+int rt_debug_probe(rt_ctx* ctx, const rt_camera* cam, int op, const double* in, int n, uint64_t seed, double* out);
+
+/*
  * Debug / numerics probe: out[i] = op(x[i], y[i]) evaluated on the device.
  * ops: 0 x/y (IEEE), 1 div_exact(x, y) (reciprocal + Markstein), 2 sqrt x, 3 sin x, 4 cos x,
  * 5 atan x, 6 asin x, 7 log x, 8 pow(x, y), 9 GHC atan2(x, y), 10 tan x, 11 the render path's

@@ -818,3 +818,78 @@ double oracle_random_double(uint64_t gen[2]) { return word_to_draw(oracle_next_w
 void oracle_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) { philox4x32_10(ctr, key, out); }
 double oracle_word_to_draw(uint64_t w) { return word_to_draw(w); }
 uint8_t oracle_scale_color(double x) { return scale_color(x); }
+
+/* ------------------------------------------------------------------ per-function probes
+ * Golden vectors for single hot-path functions (tests/golden/make_function_goldens.py).
+ * Record i is evaluated with its own tier-B Philox stream (key = seed, pid = i, sample 0), so the
+ * device probe (rt_debug_probe) consumes the same numbers. Layouts (doubles per record), in -> out:
+ *   0 scatter   (src/Lib.hs:822-865, emitted 880-885):
+ *               ray o3 d3 tm, hit t p3 n3 u v ff mat (18) -> scattered, ray o3 d3 tm, att3 (emitted
+ *               when Nothing), pdf, specular, words consumed (14)
+ *   1 htblRandom   (src/Lib.hs:707-724) on the lights tree: origin3 (3) -> direction3, words (4)
+ *   2 htblPdfValue (src/Lib.hs:673-705) on the lights tree: origin3, v3 (6) -> pdf, words (2)
+ *   3 textureValue (src/Lib.hs:496-513): texture id, u, v, p3 (6) -> albedo3 (3)
+ *   4 getRay       (src/Lib.hs:1253-1267) with `cam`: s, t (2) -> ray o3 d3 tm, words (8)
+ */
+int oracle_probe(const rt_scene_desc* scene, const rt_camera* cam, int op, const double* in, int n, uint64_t seed,
+                 double* out) {
+    static const int IN[5] = {18, 3, 6, 6, 2}, OUT[5] = {14, 4, 2, 3, 8};
+    if (!scene || op < 0 || op > 4 || n < 0 || (op == 4 && !cam)) return -1;
+    Ctx c = {scene, cam, 0, 0, 0, 0, NULL};
+    for (int i = 0; i < n; ++i) {
+        const double* q = in + (size_t)IN[op] * i;
+        double* o = out + (size_t)OUT[op] * i;
+        memset(o, 0, sizeof(double) * OUT[op]);
+        Rng g;
+        memset(&g, 0, sizeof g);
+        g.mode = RT_RNG_PHILOX;
+        g.key[0] = (uint32_t)seed;
+        g.key[1] = (uint32_t)(seed >> 32);
+        g.pid = (uint32_t)i;
+        switch (op) {
+            case 0: {
+                Ray r = {v3(q[0], q[1], q[2]), v3(q[3], q[4], q[5]), q[6]};
+                Hit h = {q[7], v3(q[8], q[9], q[10]), v3(q[11], q[12], q[13]), q[14], q[15], (int)q[16], (int)q[17]};
+                const rt_material* m = &scene->materials[h.mat];
+                Scatter s;
+                if (scatter(&c, m, r, &h, &g, &s)) {
+                    o[0] = 1;
+                    o[1] = s.ray.o.x; o[2] = s.ray.o.y; o[3] = s.ray.o.z;
+                    o[4] = s.ray.d.x; o[5] = s.ray.d.y; o[6] = s.ray.d.z; o[7] = s.ray.tm;
+                    o[8] = s.att.x; o[9] = s.att.y; o[10] = s.att.z;
+                    o[11] = s.pdf; o[12] = s.specular;
+                } else {
+                    V3 e = emitted(&c, m, &h);
+                    o[8] = e.x; o[9] = e.y; o[10] = e.z;
+                }
+                o[13] = 2.0 * g.pair - g.have_spare;
+                break;
+            }
+            case 1: {
+                V3 d = htbl_random(&c, scene->lights_root, v3(q[0], q[1], q[2]), &g);
+                o[0] = d.x; o[1] = d.y; o[2] = d.z;
+                o[3] = 2.0 * g.pair - g.have_spare;
+                break;
+            }
+            case 2:
+                o[0] = scene->lights_root < 0 ? 0.0
+                                              : htbl_pdf_value(&c, scene->lights_root, v3(q[0], q[1], q[2]),
+                                                               v3(q[3], q[4], q[5]), &g);
+                o[1] = 2.0 * g.pair - g.have_spare;
+                break;
+            case 3: {
+                V3 a = texture_value(&c, (int)q[0], q[1], q[2], v3(q[3], q[4], q[5]));
+                o[0] = a.x; o[1] = a.y; o[2] = a.z;
+                break;
+            }
+            default: {
+                Ray r = get_ray(&c, q[0], q[1], &g);
+                o[0] = r.o.x; o[1] = r.o.y; o[2] = r.o.z;
+                o[3] = r.d.x; o[4] = r.d.y; o[5] = r.d.z; o[6] = r.tm;
+                o[7] = 2.0 * g.pair - g.have_spare;
+                break;
+            }
+        }
+    }
+    return 0;
+}

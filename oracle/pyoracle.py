@@ -49,6 +49,8 @@ def lib():
         L.oracle_ghc_atan2.restype = D
         L.oracle_ghc_atan2.argtypes = [D, D]
         L.oracle_num_counters.restype = C.c_int
+        L.oracle_probe.restype = C.c_int
+        L.oracle_probe.argtypes = [C.c_void_p, C.c_void_p, C.c_int, P(D), C.c_int, U64, P(D)]
         _lib = L
     return _lib
 
@@ -86,6 +88,20 @@ def closest_hits(scene, rays, tmin, tmax, seed=0):
     P = C.POINTER
     lib().oracle_closest_hits(C.addressof(scene.desc), rays.ctypes.data_as(P(C.c_double)), rays.shape[0], tmin,
                               tmax, seed, out.ctypes.data_as(P(C.c_double)))
+    return out
+
+
+def probe(scene, op, inputs, seed=0, cam=None):
+    """oracle_probe: one hot-path function per record (layouts: oracle/oracle.c, include/rt.h)."""
+    import rtamd
+    k = rtamd.PROBES[op]
+    x = np.ascontiguousarray(inputs, dtype=np.float64).reshape(-1, rtamd.PROBE_IN[k])
+    out = np.zeros((x.shape[0], rtamd.PROBE_OUT[k]), dtype=np.float64)
+    P = C.POINTER
+    rc = lib().oracle_probe(C.addressof(scene.desc), C.addressof(cam) if cam is not None else None, k,
+                            x.ctypes.data_as(P(C.c_double)), x.shape[0], seed, out.ctypes.data_as(P(C.c_double)))
+    if rc != 0:
+        raise RuntimeError(f"oracle_probe failed ({rc})")
     return out
 
 

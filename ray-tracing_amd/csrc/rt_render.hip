@@ -751,6 +751,65 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
   }
 }
 
+// ---------------------------------------------------------------- debug: per-function probes
+// The hot-path functions one at a time on device inputs (rt_debug_probe; layouts in rt.h and
+// oracle/oracle.c oracle_probe): record i draws from its own tier-B Philox stream (key = seed, pid = i,
+// sample 0), so the oracle's golden vectors consume the same numbers.
+constexpr int kProbeIn[5] = {18, 3, 6, 6, 2}, kProbeOut[5] = {14, 4, 2, 3, 8};
+template <unsigned F>
+__global__ void __launch_bounds__(RT_BLOCK) fn_probe(Scene S, rt_camera cam, int op, const double* in, int n,
+                                                    uint64_t seed, double* out) {
+  const int i = blockIdx.x * RT_BLOCK + threadIdx.x;
+  if (i >= n) return;
+  const double* q = in + (long long)kProbeIn[op] * i;
+  double* o = out + (long long)kProbeOut[op] * i;
+  for (int k = 0; k < kProbeOut[op]; ++k) o[k] = 0.0;
+  RngPhilox g;
+  g.init(seed, (uint32_t)i, 0);
+  if (op == 0) {  // scatter (or emitted for DiffuseLight), as shade_hit runs it
+    const Ray r{v3(q[0], q[1], q[2]), v3(q[3], q[4], q[5]), q[6]};
+    Hit h;
+    h.t = q[7];
+    h.p = v3(q[8], q[9], q[10]);
+    h.n = v3(q[11], q[12], q[13]);
+    h.u = q[14];
+    h.v = q[15];
+    h.ff = (int)q[16];
+    h.mat = (int)q[17];
+    const DMat m = S.mats[h.mat];
+    if (m.type == RT_MAT_DIFFUSE_LIGHT) {
+      const V3 e = h.ff ? v3(0, 0, 0) : texture_value<F>(S, m.tex, h.u, h.v, h.p);
+      o[8] = e.x, o[9] = e.y, o[10] = e.z;
+    } else {
+      Scatter sc;
+      scatter<F>(S, m, r, h, g, sc);
+      o[0] = 1;
+      o[1] = sc.ray.o.x, o[2] = sc.ray.o.y, o[3] = sc.ray.o.z;
+      o[4] = sc.ray.d.x, o[5] = sc.ray.d.y, o[6] = sc.ray.d.z, o[7] = sc.ray.tm;
+      o[8] = sc.att.x, o[9] = sc.att.y, o[10] = sc.att.z;
+      o[11] = sc.pdf;
+      o[12] = sc.specular;
+    }
+    o[13] = g.consumed();
+  } else if (op == 1) {  // htblRandom on the lights tree
+    const V3 d = htbl_random(S, S.lights, v3(q[0], q[1], q[2]), g);
+    o[0] = d.x, o[1] = d.y, o[2] = d.z;
+    o[3] = g.consumed();
+  } else if (op == 2) {  // htblPdfValue on the lights tree
+    const V3 org = v3(q[0], q[1], q[2]), v = v3(q[3], q[4], q[5]);
+    o[0] = S.lights < 0 ? 0.0 : htbl_pdf_value<F, RT_LIGHT_DEPTH>(S, S.lights, org, v, prep(Ray{org, v, 0.0}));
+    o[1] = g.consumed();
+  } else if (op == 3) {  // textureValue
+    const V3 a = texture_value<F>(S, (int)q[0], q[1], q[2], v3(q[3], q[4], q[5]));
+    o[0] = a.x, o[1] = a.y, o[2] = a.z;
+  } else {  // getRay
+    const Ray r = get_ray(cam, q[0], q[1], g);
+    o[0] = r.o.x, o[1] = r.o.y, o[2] = r.o.z;
+    o[3] = r.d.x, o[4] = r.d.y, o[5] = r.d.z, o[6] = r.tm;
+    o[7] = g.consumed();
+  }
+}
+
 // ---------------------------------------------------------------- debug: numerics probe
 __global__ void math_probe(int op, const double* x, const double* y, int n, double* out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1684,6 +1743,29 @@ int rt_debug_closest_hits(rt_ctx* c, const double* rays, int n, double tmin, dou
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipMemcpy(out, d_out, sizeof(double) * 12 * (size_t)n, hipMemcpyDeviceToHost));
+  return RT_OK;
+}
+
+int rt_debug_probe(rt_ctx* c, const rt_camera* cam, int op, const double* in, int n, uint64_t seed, double* out) {
+  if (!c || !in || !out || n < 0 || op < 0 || op > 4 || (op == 4 && !cam)) return invalid("rt_debug_probe: bad argument");
+  if (!c->has_scene) {
+    rt::set_error("rt_debug_probe: no scene uploaded");
+    return RT_E_STATE;
+  }
+  if (n == 0) return RT_OK;
+  DEVICE_SCOPE(c->device);
+  DevBuf bin, bout;
+  const size_t nin = sizeof(double) * kProbeIn[op] * (size_t)n, nout = sizeof(double) * kProbeOut[op] * (size_t)n;
+  HIPCHK(hipMalloc(&bin.p, nin));
+  HIPCHK(hipMalloc(&bout.p, nout));
+  HIPCHK(hipMemcpy(bin.p, in, nin, hipMemcpyHostToDevice));
+  rt_camera k{};
+  if (cam) k = *cam;
+  hipLaunchKernelGGL(fn_probe<F_ALL>, dim3((n + RT_BLOCK - 1) / RT_BLOCK), dim3(RT_BLOCK), 0, c->stream, c->scene, k, op,
+                     (const double*)bin.p, n, seed, (double*)bout.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpy(out, bout.p, nout, hipMemcpyDeviceToHost));
   return RT_OK;
 }
 

@@ -39,6 +39,11 @@ RT_BVH_ORDERED = 0x40000000
 MATH_OPS = {"div": 0, "div_exact": 1, "sqrt": 2, "sin": 3, "cos": 4, "atan": 5, "asin": 6, "log": 7, "pow": 8,
             "ghc_atan2": 9, "tan": 10, "pow5": 11}
 
+# rt_debug_probe / oracle_probe: function -> op id, doubles per input / output record (rt.h)
+PROBES = {"scatter": 0, "htbl_random": 1, "htbl_pdf": 2, "texture": 3, "get_ray": 4}
+PROBE_IN = (18, 3, 6, 6, 2)
+PROBE_OUT = (14, 4, 2, 3, 8)
+
 XYPlane, XZPlane, YZPlane = 0, 1, 2
 XAxis, YAxis, ZAxis = 0, 1, 2
 RT_OK, RT_E_INVALID, RT_E_HIP, RT_E_NOMEM, RT_E_UNSUPPORTED, RT_E_STATE = 0, -1, -2, -3, -4, -5
@@ -115,7 +120,7 @@ EXPORTED = [
     "rt_device_count", "rt_create", "rt_destroy", "rt_upload_scene", "rt_render", "rt_shard_geometry",
     "rt_render_shard_async", "rt_assemble_async", "rt_assemble_linear_async", "rt_last_kernel_ms",
     "rt_debug_closest_hits", "rt_debug_math", "rt_render_work", "rt_upload_scene_ex", "rt_rebuild_bvh",
-    "rt_wide_bvh", "rt_tree_stack_need", "rt_last_launch", "rt_write_pfm",
+    "rt_wide_bvh", "rt_tree_stack_need", "rt_last_launch", "rt_write_pfm", "rt_debug_probe",
 ]
 
 # include/rt_wide.h: one 4-wide node (128 B)
@@ -193,6 +198,7 @@ def lib() -> C.CDLL:
             "rt_tree_stack_need": (I, [P(rt_node), I, I, P(I)]),
             "rt_last_launch": (I, [C.c_void_p, P(rt_launch_info)]),
             "rt_write_pfm": (I, [P(D), I, I, I, C.c_char_p, C.c_size_t, P(C.c_size_t)]),
+            "rt_debug_probe": (I, [C.c_void_p, P(rt_camera), I, P(D), I, U64, P(D)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -547,6 +553,17 @@ class Context:
         P = C.POINTER
         _check(lib().rt_debug_closest_hits(self._h, rays.ctypes.data_as(P(C.c_double)), rays.shape[0], tmin, tmax,
                                            seed, flags, out.ctypes.data_as(P(C.c_double))), "rt_debug_closest_hits")
+        return out
+
+    def probe(self, op: str, inputs: np.ndarray, seed: int = 0, cam: Optional[rt_camera] = None) -> np.ndarray:
+        """rt_debug_probe: one hot-path function per record on the device (PROBES: layouts)."""
+        k = PROBES[op]
+        x = np.ascontiguousarray(inputs, dtype=np.float64).reshape(-1, PROBE_IN[k])
+        out = np.zeros((x.shape[0], PROBE_OUT[k]), dtype=np.float64)
+        P = C.POINTER
+        _check(lib().rt_debug_probe(self._h, C.byref(cam) if cam is not None else None, k,
+                                    x.ctypes.data_as(P(C.c_double)), x.shape[0], seed,
+                                    out.ctypes.data_as(P(C.c_double))), "rt_debug_probe")
         return out
 
     def math(self, op: str, x: np.ndarray, y: Optional[np.ndarray] = None) -> np.ndarray:
