@@ -355,9 +355,14 @@ def main():
             leaf_hits, tie_redos = work.pop("leaf_hits"), work.pop("tie_redos")
             if slots["outer_iterations"]:  # lane utilisation of the replacement loop's phases
                 out["lane_utilisation"] = {"shade": round(work["segments"] / slots["outer_iterations"], 4)}
-                if slots["wide_steps"] and slots["leaf_steps"]:  # (the 4-wide walk's two kinds of step)
+                if work["wide_nodes"] and slots["wide_steps"] and slots["leaf_steps"]:  # (4-wide: two kinds of step)
                     out["lane_utilisation"]["wide_steps"] = round(work["wide_nodes"] / slots["wide_steps"], 4)
                     out["lane_utilisation"]["leaf_steps"] = round(work["prim_tests"] / slots["leaf_steps"], 4)
+                elif slots["wide_steps"]:  # binary walk: node visits per lane slot of its steps, and how many
+                    # node kinds (BVH box, leaf primitive, instance, medium) one step runs on average
+                    visits = work["box_tests"] + work["prim_tests"] + work["other_tests"]
+                    out["lane_utilisation"]["walk_steps"] = round(visits / slots["wide_steps"], 4)
+                    out["walk_step_kinds"] = round(slots["leaf_steps"] / slots["wide_steps"], 4)
             per = {k: work[k] / n for k in work}
             bytes_per_sample = sum(BYTES[k] * per[k] for k in BYTES) + 3.0 / cfg["spp"]
             flops_per_sample = sum(FLOPS[k] * per[k] for k in FLOPS)

@@ -892,16 +892,30 @@ __device__ __forceinline__ void wide_leaf(const Scene& S, Trav& t, double t_min,
 }
 
 // Step the wave's walking lanes until at most `stop` of them still walk (`walking` goes false when
-// a lane's walk is over). Binary walks: one node per lane per step. 4-wide walks: wide-node steps
-// until at most `leaf_stop` walking lanes still look for their first leaf, then one leaf step.
+// a lane's walk is over). Binary walks: one node per lane per step; while more than `leaf_stop` of
+// the walking lanes are at BVH nodes, a step runs only those (lanes at leaves, instances and media
+// wait), so that one step runs the box test alone instead of every node kind its lanes are at
+// (leaf_stop >= the live lanes: every step runs every lane). 4-wide walks: wide-node steps until at
+// most `leaf_stop` walking lanes still look for their first leaf, then one leaf step.
 template <unsigned F, class R>
 __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walking, double t_min, int* stk, int stride,
                                            bool joint, int stop, int leaf_stop, Cnt& cnt, R& g, Side& side) {
   if constexpr ((F & F_WIDE) == 0) {
-    (void)leaf_stop;
     for (;;) {
-      if (__popcll(__ballot(walking)) <= stop) break;
-      if (walking) walking = trav_step<F>(S, t, t_min, stk, stride, joint, cnt, g, side);
+      const int n_walk = __popcll(__ballot(walking));
+      if (n_walk <= stop) break;
+      const int ty = walking ? (S.nodes[kRefMixed<F> ? (t.node & ~RT_SUB) : t.node].type & RT_TYPE_MASK) : -1;
+      const bool at_box = ty == RT_NODE_BVH;
+      const bool box_only = leaf_stop < n_walk && __popcll(__ballot(at_box)) > leaf_stop;
+      if constexpr ((F & F_COUNT) != 0) {  // counting build: wave steps, and the node kinds each one runs
+        ++cnt.islot;                        // (every lane counts a step: / 64 per wave)
+        const bool inst = ty == RT_NODE_TRANSLATE || ty == RT_NODE_ROTATE;
+        const bool go = walking && (at_box || !box_only);
+        cnt.lslot += (__ballot(go && at_box) != 0) + (__ballot(go && inst) != 0) +
+                     (__ballot(go && ty == RT_NODE_CONSTANT_MEDIUM) != 0) +
+                     (__ballot(go && !at_box && !inst && ty != RT_NODE_CONSTANT_MEDIUM) != 0);
+      }
+      if (walking && (at_box || !box_only)) walking = trav_step<F>(S, t, t_min, stk, stride, joint, cnt, g, side);
     }
   } else {
     for (;;) {
