@@ -639,292 +639,6 @@ __global__ void __launch_bounds__(WAVES * 256, WAVES)
                   wave_q[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)]);
 }
 
-// ---------------------------------------------------------------- tier B, wavefront form (full variant)
-// The full variant's megakernel (media, instance frames, textures, motion: C4) carries the texture /
-// scatter code and the walk in one register allocation: 168 VGPRs with ~550 B/lane of spills at 3
-// waves per SIMD. The wavefront form splits one path segment into two kernels over a pool of P path
-// slots kept in HBM (SoA): `wf_walk` (persistent; the resumable closest-hit walk with ray
-// replacement, media draws and tie redos, no shading code) and `wf_shade` (one lane per slot:
-// the hit record, emission / scatter, the sample and chunk bookkeeping, work-item claims and
-// camera rays). Same streams, same arithmetic, same summation order as philox_loop2: the images are
-// byte-identical (tests/test_gpu_parity.py test_walks_output_identical).
-constexpr uint32_t kSlotIdle = 0xffffffffu;  // the slot needs a work-item
-constexpr uint32_t kSlotDead = 0xfffffffeu;  // no work-item is left for the slot
-
-struct WfState {
-  double* ray;      // [7][P]: o xyz, d xyz, time of the next segment (the world ray)
-  double* thr;      // [3][P]: path throughput
-  double* sum;      // [3][P]: the work-item's running chunk sum
-  uint32_t* item;   // [P]: tier-B work-item (pixel, chunk), or kSlotIdle / kSlotDead
-  int* s;           // [P]: current sample
-  int* depth;       // [P]: remaining depth of the current path
-  uint32_t* rng;    // [P]: words of sample s's Philox stream consumed so far
-  double* hit_t;    // [P]: the walk's closest hit (Trav::closest)
-  double* hit_tmax; // [P]: Trav::best_tmax (chain hits are re-run under it)
-  int* hit_node;    // [P]: Trav::best_node (-1: nothing hit)
-  int* hit_sub;     // [P]: Trav::best_sub
-  int* hit_frames;  // [1 + RT_MAX_FRAMES][P]: Trav::best_level, then the frames around the best hit
-  int P;
-  unsigned long long* walk_ctr;  // slots handed to wf_walk's lanes (reset per launch)
-  unsigned long long* live;      // slots with a segment to walk after wf_shade (reset per launch)
-};
-
-__device__ __forceinline__ Ray wf_load_ray(const WfState& W, int i) {
-  const long long P = W.P;
-  return Ray{v3(W.ray[i], W.ray[P + i], W.ray[2 * P + i]), v3(W.ray[3 * P + i], W.ray[4 * P + i], W.ray[5 * P + i]),
-             W.ray[6 * P + i]};
-}
-__device__ __forceinline__ void wf_store_ray(const WfState& W, int i, const Ray& r) {
-  const long long P = W.P;
-  W.ray[i] = r.o.x, W.ray[P + i] = r.o.y, W.ray[2 * P + i] = r.o.z;
-  W.ray[3 * P + i] = r.d.x, W.ray[4 * P + i] = r.d.y, W.ray[5 * P + i] = r.d.z;
-  W.ray[6 * P + i] = r.tm;
-}
-__device__ __forceinline__ V3 wf_load3(const double* a, long long P, int i) { return v3(a[i], a[P + i], a[2 * P + i]); }
-__device__ __forceinline__ void wf_store3(double* a, long long P, int i, V3 v) {
-  a[i] = v.x, a[P + i] = v.y, a[2 * P + i] = v.z;
-}
-__device__ __forceinline__ uint32_t item_pid(const RenderArgs& A, uint32_t item, int& px, int& row, int& s0, int& s1,
-                                             long long& slot) {
-  work_item(A, item, px, row, s0, s1, slot);
-  return (uint32_t)((long long)row * A.W + px);
-}
-
-// One walk per claimed slot; lanes whose walk has ended store its result and take the next slot while
-// the others keep stepping (walk_until), as in philox_loop2.
-template <unsigned F>
-__device__ __forceinline__ void wf_walk_loop(const RenderArgs& A, const Scene& S, const WfState& W, int* stk,
-                                             int stride, int* side_p, volatile uint32_t* wq) {
-  const int lane = threadIdx.x & 63;
-  const unsigned long long lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const bool joint = !(A.flags & RT_FLAG_REFERENCE_CULL);
-  if (lane == 0) {
-    wq[0] = 0u;
-    wq[1] = 0u;
-  }
-  int slot = -1;
-  bool done = false, walking = false;
-  uint32_t walk_mark = 0;
-  RngPhilox g;
-  g.init(A.seed, 0, 0);
-  Trav t;
-  Side side{side_p, stride};
-  Cnt cnt{};
-  const long long total = W.P;
-  for (;;) {
-    if (slot >= 0 && !walking) {
-      if (t.tie && !t.redo) {  // exact tie: redo this walk as the reference does (once)
-        g.rewind(walk_mark);
-        trav_restart_ref(t, S.world_ref, INFINITY, true);
-        walking = true;
-      } else {  // the walk's result, for wf_shade
-        const long long P = W.P;
-        W.hit_t[slot] = t.closest;
-        W.hit_tmax[slot] = t.best_tmax;
-        W.hit_node[slot] = t.best_node;
-        W.hit_sub[slot] = t.best_sub;
-        if constexpr ((F & F_FRAMES) != 0) {
-          W.hit_frames[slot] = t.best_level;
-          for (int k = 0; k < t.best_level; ++k) W.hit_frames[(k + 1) * P + slot] = side.best(k);
-        }
-        W.rng[slot] = g.consumed();
-        slot = -1;
-      }
-    }
-    // idle lanes take the next slots with a segment to walk (batched claims, as philox_loop2)
-    for (;;) {
-      const bool need = slot < 0 && !done;
-      const unsigned long long mask = __ballot(need);
-      if (!mask) break;
-      const uint32_t n_need = (uint32_t)__popcll(mask);
-      const uint32_t q_next = wq[0], q_end = wq[1];
-      const uint32_t avail = q_end - q_next;
-      uint32_t base2 = q_next, end2 = q_end;
-      const int leader = __ffsll((long long)mask) - 1;
-      if (avail < n_need) {
-        unsigned long long claim = 0;
-        if (lane == leader) {
-          const uint32_t want = n_need - avail;
-          const long long rem = total - (long long)q_end;
-          const uint32_t b = rem <= 0 ? 0u : (uint32_t)fminf((float)A.batch, (float)rem * A.batch_per_item);
-          const uint32_t got = want < b ? b : want;
-          const unsigned long long c0 = atomicAdd(W.walk_ctr, (unsigned long long)got);
-          claim = (c0 < 0xffff0000ull ? c0 : 0xffff0000ull) | ((unsigned long long)got << 32);
-        }
-        const unsigned long long c1 = __shfl(claim, leader);
-        base2 = (uint32_t)c1;
-        end2 = base2 + (uint32_t)(c1 >> 32);
-      }
-      const uint32_t rank = (uint32_t)__popcll(mask & lanes_below);
-      if (need) {
-        const long long i = (long long)(rank < avail ? q_next + rank : base2 + (rank - avail));
-        if (i >= total) {
-          done = true;
-        } else {
-          const uint32_t item = W.item[i];
-          if (item < kSlotDead) {  // a segment to walk: its ray and stream position
-            int px, row, s0, s1;
-            long long ps;
-            const uint32_t pid = item_pid(A, item, px, row, s0, s1, ps);
-            g.init(A.seed, pid, (uint32_t)W.s[i]);
-            g.rewind(W.rng[i]);
-            const Ray r = wf_load_ray(W, (int)i);
-            trav_begin<F>(t, r, S.world, kEps, INFINITY);
-            if (S.ref_walk) trav_restart_ref(t, S.world, INFINITY);
-            walk_mark = g.consumed();
-            if constexpr ((F & F_MEDIA) != 0) g.reserve(2);
-            walking = true;
-            slot = (int)i;
-          }
-        }
-      }
-      if (lane == leader) {
-        wq[0] = avail < n_need ? base2 + (n_need - avail) : q_next + n_need;
-        wq[1] = end2;
-      }
-    }
-    if (!walking) break;  // no slot left for this lane
-    const int live = __popcll(__ballot(true));
-    walk_until<F>(S, t, walking, kEps, stk, stride, joint, (live * A.trav_stop) >> 6,
-                  (live * ((F & F_WIDE) ? A.leaf_stop : A.box_first)) >> 6, cnt, g, side);
-  }
-}
-
-template <unsigned F, int WAVES>
-__global__ void __launch_bounds__(RT_BLOCK, WAVES) wf_walk(RenderArgs A, WfState W, int stack_entries) {
-  extern __shared__ __attribute__((aligned(16))) int stk_mem[];
-  __shared__ uint32_t wave_q[RT_BLOCK / 64][2];
-  // (the live-slot count is wf_shade's, read by the host after it: the next shade counts afresh)
-  if (blockIdx.x == 0 && threadIdx.x == 0) *W.live = 0;
-  wf_walk_loop<F>(A, A.S, W, &stk_mem[threadIdx.x], RT_BLOCK, &stk_mem[stack_entries * RT_BLOCK + threadIdx.x],
-                  wave_q[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)]);
-}
-
-// One lane per slot: shade the walked segment (rayColor's continuation, Lib.hs:1309-1333); a path
-// that ends adds its sample to the chunk sum and starts the next sample (getRay after the UV pair),
-// a chunk that ends stores its sum and the slot claims the next work-item.
-constexpr int kShadeBlock = 256;
-template <unsigned F>
-__global__ void __launch_bounds__(kShadeBlock) wf_shade(RenderArgs A, WfState W) {
-  extern __shared__ __attribute__((aligned(16))) int side_mem[];  // (F_FRAMES) Side slots per lane
-  // (the walk kernel's slot counter: the next wf_walk claims from 0 again)
-  if (blockIdx.x == 0 && threadIdx.x == 0) *W.walk_ctr = 0;
-  const int i = blockIdx.x * kShadeBlock + threadIdx.x;
-  const int lane = threadIdx.x & 63;
-  const unsigned long long lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const long long P = W.P;
-  const Scene& S = A.S;
-  uint32_t item = i < W.P ? W.item[i] : kSlotDead;
-  int px = 0, row = 0, s0 = 0, s1 = 0, s = 0, depth = 0;
-  long long pslot = 0;
-  V3 thr = v3(0, 0, 0), sum = v3(0, 0, 0);
-  Ray ray{};
-  RngPhilox g;
-  g.init(A.seed, 0, 0);
-  Cnt cnt{};
-  bool live = false, need = item == kSlotIdle, sum_dirty = false;
-  // sample s is over: add its colour; the chunk is done after its last sample
-  auto end_sample = [&](V3 contrib) __attribute__((always_inline)) {
-    if (A.flags & RT_FLAG_NAN_ZERO) contrib = nan_zero(contrib);
-    sum = sum + contrib;
-    sum_dirty = true;
-    ++s;
-    const bool all_nan = (A.flags & RT_FLAG_NAN_CULL) && sum.x != sum.x && sum.y != sum.y && sum.z != sum.z;
-    if (s == s1 || all_nan) {
-      store_partial(A, pslot, sum);
-      need = true;
-      sum_dirty = false;
-    }
-  };
-  if (item < kSlotDead) {
-    const uint32_t pid = item_pid(A, item, px, row, s0, s1, pslot);
-    s = W.s[i];
-    depth = W.depth[i];
-    g.init(A.seed, pid, (uint32_t)s);
-    g.rewind(W.rng[i]);
-    ray = wf_load_ray(W, i);
-    thr = wf_load3(W.thr, P, i);
-    Trav t;
-    t.best_node = W.hit_node[i];
-    t.best_sub = W.hit_sub[i];
-    t.closest = W.hit_t[i];
-    t.best_tmax = W.hit_tmax[i];
-    t.best_level = 0;
-    Side side{side_mem + threadIdx.x, kShadeBlock};
-    if constexpr ((F & F_FRAMES) != 0) {
-      t.best_level = W.hit_frames[i];
-      for (int k = 0; k < t.best_level; ++k) side.best(k) = W.hit_frames[(k + 1) * P + i];
-    }
-    Hit h;
-    const bool got = trav_finish<F>(S, t, ray, kEps, h, side);
-    V3 contrib;
-    if (shade_hit<F>(S, got, h, ray, thr, depth, g, contrib, cnt)) {
-      sum = wf_load3(W.sum, P, i);
-      end_sample(contrib);
-    } else if (depth <= 0) {  // rayColor's d <= 0 -> black (thr * 0 keeps a NaN throughput NaN)
-      sum = wf_load3(W.sum, P, i);
-      end_sample(vmul(thr, v3(0.0, 0.0, 0.0)));
-    } else {
-      live = true;  // next segment of the same path (ray and thr updated by shade_hit)
-    }
-  }
-  // start the next sample of the chunk, or claim work-items until the slot has a segment to walk
-  for (;;) {
-    if (!live && !need && item < kSlotDead) {  // the chunk goes on: start sample s
-      for (;;) {
-        g.init(A.seed, (uint32_t)((long long)row * A.W + px), (uint32_t)s);
-        g.reserve(3);  // the UV pair and the first disk try
-        const double ru = g.draw(), rv = g.draw();
-        const int y = A.H - 1 - row;
-        const double u = ((double)px + ru) / (double)A.W;
-        const double v = ((double)y + rv) / (double)A.H;
-        ray = get_ray(A.cam, u, v, g);
-        thr = v3(1.0, 1.0, 1.0);
-        depth = A.max_depth;
-        if (depth > 0) {
-          live = true;
-          break;
-        }
-        end_sample(vmul(thr, v3(0.0, 0.0, 0.0)));
-        if (need) break;
-      }
-    }
-    const unsigned long long mask = __ballot(need);
-    if (!mask) break;
-    const int leader = __ffsll((long long)mask) - 1;
-    unsigned long long base = 0;
-    if (lane == leader) base = atomicAdd(A.counter, (unsigned long long)__popcll(mask));
-    base = __shfl(base, leader);
-    if (need) {
-      need = false;
-      const long long wi = (long long)(base + __popcll(mask & lanes_below));
-      if (wi >= A.work_total) {
-        item = kSlotDead;
-      } else if (work_item(A, (uint32_t)wi, px, row, s0, s1, pslot)) {
-        item = (uint32_t)wi;
-        s = s0;
-        sum = v3(0, 0, 0);
-        sum_dirty = true;
-      } else {
-        need = true;  // (a padding pixel outside the image: claim another)
-      }
-    }
-  }
-  if (i < W.P) {
-    W.item[i] = item;
-    if (live) {
-      W.s[i] = s;
-      W.depth[i] = depth;
-      W.rng[i] = g.consumed();
-      wf_store_ray(W, i, ray);
-      wf_store3(W.thr, P, i, thr);
-    }
-    if (sum_dirty) wf_store3(W.sum, P, i, sum);
-  }
-  const unsigned long long lm = __ballot(live);
-  if (lane == __ffsll((long long)(__ballot(true))) - 1 && lm) atomicAdd(W.live, (unsigned long long)__popcll(lm));
-}
-
 // Tier B: a slab pixel's chunk sums added in chunk order, then averaged and stored (rt.h).
 __global__ void __launch_bounds__(256) combine_chunks(RenderArgs A) {
   const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -1159,12 +873,6 @@ struct rt_ctx {
   size_t partial_bytes = 0;
   double last_ms = 0.0;
   rt_launch_info last_launch{};  // rt_last_launch
-  // wavefront form (full variant): the path-slot pool (one allocation), its size, and the host side
-  // of the live-slot polls
-  void* d_wf = nullptr;
-  size_t wf_bytes = 0;
-  unsigned long long* h_live = nullptr;  // pinned, 2 words (polls in flight alternate)
-  hipEvent_t ev_poll[2] = {nullptr, nullptr};
 };
 
 namespace {
@@ -1510,97 +1218,6 @@ int launch_combine(rt_ctx* c, const RenderArgs& A, hipStream_t st) {
   return RT_OK;
 }
 
-// Wavefront form (full variant): wf_shade fills the slots with camera rays, then
-// wf_walk / wf_shade alternate until no slot has a segment left. The live-slot count is polled every
-// kWfBatch iterations, one batch behind (the next batch is queued before the host waits), so the
-// device never waits for the host; launches after the last segment find every slot dead and exit.
-constexpr int kWfBatch = 8;
-size_t wf_slot_bytes() { return sizeof(double) * (7 + 3 + 3 + 2) + sizeof(int) * (6 + 1 + RT_MAX_FRAMES); }
-template <unsigned V>
-const void* wf_walk_kernel(int waves) {
-  return waves >= 4 ? (const void*)wf_walk<V, 4> : (waves == 3 ? (const void*)wf_walk<V, 3> : (const void*)wf_walk<V, 2>);
-}
-int launch_wavefront(rt_ctx* c, RenderArgs& A, unsigned var, hipStream_t st) {
-  const char* pe = std::getenv("RTAMD_WF_SLOTS");
-  long long P = pe ? std::atoll(pe) : (1ll << 21);
-  P = std::max(256ll, std::min(P, ((A.work_total + 255) / 256) * 256));
-  const size_t need = (size_t)P * wf_slot_bytes();
-  if (need > c->wf_bytes) {
-    HIPCHK(hipEventSynchronize(c->ev_done));
-    (void)hipFree(c->d_wf);
-    c->d_wf = nullptr;
-    c->wf_bytes = 0;
-    HIPCHK(hipMalloc(&c->d_wf, need));
-    c->wf_bytes = need;
-  }
-  if (!c->h_live) {
-    HIPCHK(hipHostMalloc((void**)&c->h_live, 2 * sizeof(unsigned long long), hipHostMallocDefault));
-    for (auto& e : c->ev_poll) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  }
-  WfState W{};
-  {
-    char* b = (char*)c->d_wf;
-    auto take = [&](size_t bytes) { char* r = b; b += bytes; return r; };
-    W.ray = (double*)take(sizeof(double) * 7 * P);
-    W.thr = (double*)take(sizeof(double) * 3 * P);
-    W.sum = (double*)take(sizeof(double) * 3 * P);
-    W.hit_t = (double*)take(sizeof(double) * P);
-    W.hit_tmax = (double*)take(sizeof(double) * P);
-    W.item = (uint32_t*)take(sizeof(uint32_t) * P);
-    W.s = (int*)take(sizeof(int) * P);
-    W.depth = (int*)take(sizeof(int) * P);
-    W.rng = (uint32_t*)take(sizeof(uint32_t) * P);
-    W.hit_node = (int*)take(sizeof(int) * P);
-    W.hit_sub = (int*)take(sizeof(int) * P);
-    W.hit_frames = (int*)take(sizeof(int) * (1 + RT_MAX_FRAMES) * P);
-    W.P = (int)P;
-    W.walk_ctr = c->d_counter + 1;
-    W.live = c->d_counter + 2;
-  }
-  HIPCHK(hipMemsetAsync(W.item, 0xff, sizeof(uint32_t) * P, st));  // every slot kSlotIdle
-  HIPCHK(hipMemsetAsync(c->d_counter + 1, 0, 2 * sizeof(unsigned long long), st));
-  // walk kernel: dynamic LDS stacks (+ Side slots) as the replacement loop's; waves per SIMD
-  // RTAMD_WF_WAVES (default 3)
-  const int wwaves = std::max(2, std::min(4, std::getenv("RTAMD_WF_WAVES") ? std::atoi(std::getenv("RTAMD_WF_WAVES")) : 3));
-  const void* fw = var == kVarFullDark ? wf_walk_kernel<kVarFullDark>(wwaves) : wf_walk_kernel<F_ALL>(wwaves);
-  const void* fs = var == kVarFullDark ? (const void*)wf_shade<kVarFullDark> : (const void*)wf_shade<F_ALL>;
-  int entries = c->stack_need + 2;
-  const size_t dyn_w = (size_t)(entries + kSideInts) * RT_BLOCK * sizeof(int);
-  const size_t dyn_s = (size_t)kSideInts * kShadeBlock * sizeof(int);
-  HIPCHK(hipFuncSetAttribute(fw, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn_w));
-  HIPCHK(hipFuncSetAttribute(fs, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn_s));
-  int bpc = 1;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fw, RT_BLOCK, dyn_w));
-  const int grid_w = (int)std::max(1ll, std::min((P + RT_BLOCK - 1) / RT_BLOCK, (long long)c->cu_count * std::max(1, bpc)));
-  const int grid_s = (int)((P + kShadeBlock - 1) / kShadeBlock);
-  c->last_launch = rt_launch_info{var, 3, 0, 0, wwaves, grid_w, RT_BLOCK, (int)dyn_w, A.work_total, A.chunk, 0};
-  void* aw[] = {&A, &W, &entries};
-  void* as[] = {&A, &W};
-  HIPCHK(hipEventRecord(c->ev0, st));
-  HIPCHK(hipLaunchKernel(fs, dim3(grid_s), dim3(kShadeBlock), as, dyn_s, st));  // camera rays into every slot
-  // (a hang guard: every iteration advances each live path by one segment, so a frame takes about
-  // ceil(items / P) * chunk * (segments per sample) iterations; 64x the depth-bound worst case of
-  // that is never reached by a working loop)
-  const long long max_batches =
-      64 * ((A.work_total + P - 1) / P) * (long long)A.chunk * (A.max_depth + 1) / kWfBatch + 64;
-  for (long long batch = 0;; ++batch) {
-    if (batch > max_batches) return invalid("wavefront: the frame did not finish (internal error)");
-    for (int k = 0; k < kWfBatch; ++k) {
-      HIPCHK(hipLaunchKernel(fw, dim3(grid_w), dim3(RT_BLOCK), aw, dyn_w, st));
-      HIPCHK(hipLaunchKernel(fs, dim3(grid_s), dim3(kShadeBlock), as, dyn_s, st));
-    }
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(&c->h_live[batch & 1], W.live, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipEventRecord(c->ev_poll[batch & 1], st));
-    if (batch > 0) {  // the previous batch's count (this batch is already queued behind it)
-      HIPCHK(hipEventSynchronize(c->ev_poll[(batch - 1) & 1]));
-      if (c->h_live[(batch - 1) & 1] == 0) break;
-    }
-  }
-  HIPCHK(hipEventRecord(c->ev1, st));
-  return launch_combine(c, A, st);
-}
-
 int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int rank, int shards, uint8_t* d_rgb,
                   double* d_lin, hipStream_t st, unsigned long long* d_work = nullptr) {
   RenderArgs A{};
@@ -1694,10 +1311,6 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   // replacement loop 3 (C3 359.6 ms vs 374.3 at 4, 453.3 at 2), 1 on the per-sample loop; full
   // variant on the replacement loop 3 (C4 at 100 spp: 90.9 vs 87.5 Msamples/s at 2), on the
   // per-sample loop 2 despite 784 B/lane of scratch (C4 35.2 vs 23.4 at 1 wave, 9.1 at 3)
-  // Full variant on the replacement loop: the wavefront form (RTAMD_WAVEFRONT=1) splits walk and
-  // shading into two kernels over a slot pool in HBM (launch_wavefront).
-  if (!count && loop == 1 && is_full(var) && std::getenv("RTAMD_WAVEFRONT") && std::getenv("RTAMD_WAVEFRONT")[0] == '1')
-    return launch_wavefront(c, A, var, st);
   int waves = (var == kVarSpheres || loop) ? waves_target(3) : waves_target(is_full(var) ? 2 : 1);
   const int side_ints = (var & F_FRAMES) && loop == 1 ? kSideInts : 0;  // Side slots after the stacks
   // LDS-staged kernel when the traversal's node array plus the stacks fit one CU's 160 KiB
@@ -1802,10 +1415,6 @@ void rt_destroy(rt_ctx* c) {
   free_scene(c);
   (void)hipFree(c->d_counter);
   (void)hipFree(c->d_partial);
-  (void)hipFree(c->d_wf);
-  if (c->h_live) (void)hipHostFree(c->h_live);
-  for (auto& e : c->ev_poll)
-    if (e) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ev_done) (void)hipEventDestroy(c->ev_done);

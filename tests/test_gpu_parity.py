@@ -368,27 +368,3 @@ def test_run_render_zip_truncation(gpu_ctx):
     assert all(np.array_equal(a, b[:41]) for a, b in zip(short, full))
     assert all(np.array_equal(a, b) for a, b in zip(rtamd.runRender(env, gens, ctx=gpu_ctx), full))
     assert all(r.shape == (0, 3) for r in rtamd.runRender(env, [], ctx=gpu_ctx))
-
-
-@pytest.mark.parametrize("name,cam,slots", [("next_week_final", "next_week", "0"), ("next_week_final", "next_week", "512"),
-                                            ("cornell_smoke", "cornell", "0"), ("cornell_smoke", "cornell", "300")])
-def test_wavefront_form_output_identical(gpu_ctx, name, cam, slots, monkeypatch):
-    """The full variant's wavefront form (wf_walk + wf_shade over a slot pool in HBM) and its
-    megakernel give byte- and bit-identical images (same streams, arithmetic and summation order),
-    with the default pool and with a pool much smaller than the frame (slots reused for many
-    work-items, many poll batches)."""
-    earth = np.load(_earth_path())["rgb"] if name == "next_week_final" else None
-    sc, _ = _scene(name, earth=earth)
-    c = rtamd.camera(cam, 96, 64)
-    gpu_ctx.upload(sc)
-    p = rtamd.make_params(96, 64, 6, 50, rtamd.RT_RNG_PHILOX, seed=23)
-    monkeypatch.setenv("RTAMD_WAVEFRONT", "0")
-    rgb_m, lin_m, _ = gpu_ctx.render(c, p, linear=True)
-    monkeypatch.setenv("RTAMD_WAVEFRONT", "1")
-    if slots != "0":
-        monkeypatch.setenv("RTAMD_WF_SLOTS", slots)
-    rgb_w, lin_w, _ = gpu_ctx.render(c, p, linear=True)
-    info = gpu_ctx.last_launch()
-    print(f"{name} slots {slots}: launch {info}")
-    assert info["loop"] == 3
-    assert np.array_equal(rgb_w, rgb_m) and np.array_equal(lin_w, lin_m, equal_nan=True)
