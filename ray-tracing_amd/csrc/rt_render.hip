@@ -1290,8 +1290,11 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   // leaf steps once <= that many lanes still seek their first leaf (measured: C2 212.6 ms at 6-8/64
   // vs 219.7 at 0 and 232 without postponement; C5 (16 spp) 219.9 ms at 16/64 vs 326 at 0)
   A.leaf_stop = leaf_env ? std::max(0, std::min(64, std::atoi(leaf_env))) : A.trav_stop;
+  // binary walks of the full variant (media / frame worlds, C4): box-only steps while more than
+  // box_first/64 of the live lanes are at BVH nodes (measured on C4 at 100 spp: 64 (never) 430 ms,
+  // 48 416, 32 406, 16 398, 8 413; C3's Cornell kernel does not take it)
   const char* box_env = std::getenv("RTAMD_BOX_FIRST");
-  A.box_first = box_env ? std::max(0, std::min(64, std::atoi(box_env))) : 64;
+  A.box_first = box_env ? std::max(0, std::min(64, std::atoi(box_env))) : 16;
   const unsigned var = variant_for(c->features);
   const bool count = d_work != nullptr;
   // Replacement loop (RTAMD_REPLACE=0 disables) for every world whose instance frames nest at most

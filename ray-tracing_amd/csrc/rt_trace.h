@@ -904,9 +904,13 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
     for (;;) {
       const int n_walk = __popcll(__ballot(walking));
       if (n_walk <= stop) break;
-      const int ty = walking ? (S.nodes[kRefMixed<F> ? (t.node & ~RT_SUB) : t.node].type & RT_TYPE_MASK) : -1;
+      // (box-first steps only in the full variant's kernels, whose steps mix node kinds; elsewhere the
+      // node-kind read and ballots would be overhead: C3 357 ms either way)
+      constexpr bool kBoxFirst = kRefMixed<F> || (F & F_COUNT) != 0;
+      const int ty = (kBoxFirst && walking) ? (S.nodes[kRefMixed<F> ? (t.node & ~RT_SUB) : t.node].type & RT_TYPE_MASK)
+                                            : -1;
       const bool at_box = ty == RT_NODE_BVH;
-      const bool box_only = leaf_stop < n_walk && __popcll(__ballot(at_box)) > leaf_stop;
+      const bool box_only = kBoxFirst && leaf_stop < n_walk && __popcll(__ballot(at_box)) > leaf_stop;
       if constexpr ((F & F_COUNT) != 0) {  // counting build: wave steps, and the node kinds each one runs
         ++cnt.islot;                        // (every lane counts a step: / 64 per wave)
         const bool inst = ty == RT_NODE_TRANSLATE || ty == RT_NODE_ROTATE;
@@ -915,7 +919,7 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
                      (__ballot(go && ty == RT_NODE_CONSTANT_MEDIUM) != 0) +
                      (__ballot(go && !at_box && !inst && ty != RT_NODE_CONSTANT_MEDIUM) != 0);
       }
-      if (walking && (at_box || !box_only)) walking = trav_step<F>(S, t, t_min, stk, stride, joint, cnt, g, side);
+      if (walking && (!box_only || at_box)) walking = trav_step<F>(S, t, t_min, stk, stride, joint, cnt, g, side);
     }
   } else {
     for (;;) {
