@@ -1,0 +1,898 @@
+// rt_kernels.h — the render kernels as templates (device code), shared by the kernel translation
+// units: rt_k_spheres.hip, rt_k_cornell.hip and rt_k_full.hip each instantiate one scene
+// variant's render kernels (so the variants compile in parallel), rt_render.hip the small kernels
+// and the host half of the C ABI. Kernel design: DESIGN.md §3.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rt.h"
+#include "rt_device.h"
+#include "rt_internal.h"
+#include "rt_trace.h"
+
+using namespace rtd;
+
+namespace {
+
+// Wave-level timestamp for the counting build's phase split (MI355X_MICROARCH.md / HIP guide
+// "In-kernel stamps": one asm statement with its own lgkmcnt wait, fenced by sched barriers).
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
+// Unsigned 32-bit division by an invariant divisor d >= 1 (Granlund & Montgomery): with
+// l = ceil(log2 d) and m = floor(2^32 (2^l - d) / d) + 1, n / d = (t + ((n - t) >> s1)) >> s2 for
+// every 32-bit n, t = umulhi(m, n), s1 = min(l, 1), s2 = max(l - 1, 0). One multiply and a few
+// shifts instead of the software division a `/` on the device becomes.
+struct UDiv {
+  uint32_t m;
+  int s1, s2;
+};
+inline UDiv make_udiv(uint32_t d) {
+  int l = 0;
+  while ((1ull << l) < d) ++l;
+  const uint64_t m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
+  return UDiv{(uint32_t)m, l < 1 ? l : 1, l > 1 ? l - 1 : 0};
+}
+__device__ __forceinline__ uint32_t udiv(uint32_t n, UDiv d) {
+  const uint32_t t = __umulhi(d.m, n);
+  return (t + ((n - t) >> d.s1)) >> d.s2;
+}
+
+struct RenderArgs {
+  Scene S;
+  rt_camera cam;
+  int W, H, spp, max_depth;
+  uint32_t flags;
+  int tile, tiles_x, tiles_total, shard_rank, shard_count;
+  long long work_total;  // work-items of this shard: slab pixels x sample chunks (< 2^32)
+  long long slab;        // slab pixels of this shard
+  int chunk, chunks;     // tier B: samples per chunk (rt_sample_chunk) and chunks per pixel
+  UDiv div_tp, div_tile, div_tiles_x, div_bpr;  // by tile*tile, tile*tile*chunks, tiles_x, tile/8
+  double* partial;       // tier B: chunk sums, [chunk][slab pixel][3]
+  uint64_t seed;
+  unsigned long long* counter;
+  unsigned long long* work;  // counting build: [segments, box, prim, other, light, blocks, samples]
+  int trav_stop;             // replacement loop: keep stepping while > trav_stop/64 of live lanes walk
+  int batch;                 // replacement loop: most work-items a wave claims per atomic
+  float batch_per_item;      // ...tapering to rem * batch_per_item as `rem` items remain (>= need)
+  int leaf_stop;             // 4-wide walk: leaf step once <= leaf_stop/64 of live lanes seek a leaf
+  int box_first;             // binary walk: box-only steps while > box_first/64 of live lanes are at BVH
+                             // nodes (64: never)
+  uint8_t* out_rgb;  // tier B: slab; tier A: image
+  double* out_lin;
+  uint64_t* gens;  // tier A: per-column (seed, gamma), updated in place
+};
+
+// Slab pixel index -> image pixel (tile-major, 8x8 blocks inside a tile). Slab indices are < 2^32
+// (launch_philox checks).
+__device__ __forceinline__ bool work_pixel(const RenderArgs& A, uint32_t w, int& px, int& row) {
+  const uint32_t tp = (uint32_t)(A.tile * A.tile);
+  const uint32_t lt = udiv(w, A.div_tp);
+  const uint32_t within = w - lt * tp;
+  const long long gt = (long long)A.shard_rank + (long long)lt * A.shard_count;
+  if (gt >= A.tiles_total) return false;
+  const uint32_t ty = udiv((uint32_t)gt, A.div_tiles_x), tx = (uint32_t)gt - ty * (uint32_t)A.tiles_x;
+  const uint32_t blk = within >> 6, l = within & 63;
+  const uint32_t by = udiv(blk, A.div_bpr), bx = blk - by * (uint32_t)(A.tile >> 3);
+  px = (int)(tx * A.tile + bx * 8 + (l & 7));
+  row = (int)(ty * A.tile + by * 8 + (l >> 3));
+  return px < A.W && row < A.H;
+}
+
+// Tier-B work-item -> (slab pixel, sample chunk). Items run tile by tile, chunk by chunk inside a
+// tile, so a wave's 64 consecutive items are one 8x8 pixel block at one chunk (coherent rays).
+// Returns false for pixels outside the image; else the sample range [s0, s1) and the chunk
+// sum's slot in `partial`.
+__device__ __forceinline__ bool work_item(const RenderArgs& A, uint32_t wi, int& px, int& row, int& s0, int& s1,
+                                          long long& slot) {
+  const uint32_t tp = (uint32_t)(A.tile * A.tile);
+  const uint32_t lt = udiv(wi, A.div_tile);  // by tp * chunks
+  const uint32_t rem = wi - lt * tp * (uint32_t)A.chunks;
+  const uint32_t k = udiv(rem, A.div_tp);
+  const uint32_t idx = lt * tp + (rem - k * tp);
+  if (!work_pixel(A, idx, px, row)) return false;
+  s0 = (int)k * A.chunk;
+  s1 = min(A.spp, s0 + A.chunk);
+  slot = (long long)k * A.slab + idx;
+  return s0 < s1;
+}
+__device__ __forceinline__ void store_partial(const RenderArgs& A, long long slot, V3 sum) {
+  double* q = A.partial + slot * 3;
+  q[0] = sum.x;
+  q[1] = sum.y;
+  q[2] = sum.z;
+}
+
+// getRay (Lib.hs:1253-1267): the disk and time draws always happen.
+template <class R>
+__device__ __forceinline__ Ray get_ray(const rt_camera& k, double s, double t, R& g) {
+  const V3 rd = scale(k.lens_radius, random_in_unit_disk(g));
+  const V3 offset = scale(rd.x, vload(k.u)) + scale(rd.y, vload(k.v));
+  g.reserve(1);
+  const double tm = draw_r(g, k.t0, k.t1);
+  Ray r;
+  r.o = vload(k.origin) + offset;
+  r.d = (((vload(k.llc) + scale(s, vload(k.horiz))) + scale(t, vload(k.vert))) - vload(k.origin)) - offset;
+  r.tm = tm;
+  return r;
+}
+
+// scaleColor (Lib.hs:287-288): NaN -> 0, +inf -> 255.
+__device__ __forceinline__ uint8_t scale_color(double x) {
+  const double s = sqrt(x);
+  const double cl = s < 0.0 ? 0.0 : (s > 0.999 ? 0.999 : s);
+  const double f = floor(256 * cl);
+  return f == f ? (uint8_t)(int)f : (uint8_t)0;
+}
+
+// RT_FLAG_NAN_ZERO (parity diagnostic, rt.h): a NaN channel of a sample's colour adds 0
+__device__ __forceinline__ V3 nan_zero(V3 a) {
+  return v3(a.x != a.x ? 0.0 : a.x, a.y != a.y ? 0.0 : a.y, a.z != a.z ? 0.0 : a.z);
+}
+
+__device__ __forceinline__ void store_pixel(const RenderArgs& A, long long idx, V3 avg) {
+  A.out_rgb[idx * 3 + 0] = scale_color(avg.x);
+  A.out_rgb[idx * 3 + 1] = scale_color(avg.y);
+  A.out_rgb[idx * 3 + 2] = scale_color(avg.z);
+  if (A.out_lin) {
+    A.out_lin[idx * 3 + 0] = avg.x;
+    A.out_lin[idx * 3 + 1] = avg.y;
+    A.out_lin[idx * 3 + 2] = avg.z;
+  }
+}
+
+// One path segment: closest hit, then emission/background or a scatter. Returns true when the
+// path ends, with its contribution in `contrib` (rayColor, Lib.hs:1298-1333).
+template <unsigned F, class R>
+__device__ __forceinline__ bool segment(const RenderArgs& A, const Scene& S, Ray& ray, V3& thr, int& depth, R& g,
+                                        int* stk, V3& contrib, Cnt& cnt, int stride = RT_BLOCK,
+                                        unsigned long long* t_trav = nullptr) {
+  if (depth <= 0) {  // d <= 0 -> black
+    contrib = vmul(thr, v3(0.0, 0.0, 0.0));
+    return true;
+  }
+  Hit h;
+  // (worlds walked in the reference's order: the recursive walk takes the caller's tree as is)
+  const bool got = traverse<F>(S, S.ref_walk ? S.world_ref : S.world, ray, kEps, INFINITY, h, g, stk,
+                               !(A.flags & RT_FLAG_REFERENCE_CULL), cnt, stride);
+  if constexpr ((F & F_COUNT) != 0) *t_trav = stamp();
+  if (!got) {
+    contrib = vmul(thr, v3(S.bg[0], S.bg[1], S.bg[2]));
+    return true;
+  }
+  const DMat m = S.mats[h.mat];
+  if (m.type == RT_MAT_DIFFUSE_LIGHT) {  // scatter -> Nothing: emitted (Lib.hs:880-885)
+    const V3 e = h.ff ? v3(0, 0, 0) : texture_value<F>(S, m.tex, h.u, h.v, h.p);
+    contrib = vmul(thr, e);
+    return true;
+  }
+  Scatter s;
+  if constexpr ((F & F_COUNT) != 0) cnt.light += (m.type == RT_MAT_LAMBERTIAN && S.lights >= 0);
+  scatter<F>(S, m, ray, h, g, s);
+  if (s.specular) {
+    thr = vmul(thr, s.att);
+  } else {
+    const double c = dot(h.n, s.ray.d);  // scatteringPdf (Lib.hs:874-878)
+    const double spdf = c < 0 ? 0 : c / kPi;
+    const double k = spdf / s.pdf;
+    thr = vmul(thr, scale(k, s.att));
+  }
+  ray = s.ray;
+  --depth;
+  return false;
+}
+
+// The rest of a segment once its closest hit is known (rayColor, Lib.hs:1309-1333): background,
+// emission, or a scatter. Returns true when the path ends (contribution in `contrib`).
+template <unsigned F, class R>
+__device__ __forceinline__ bool shade_hit(const Scene& S, bool got, const Hit& h, Ray& ray, V3& thr, int& depth, R& g,
+                                          V3& contrib, Cnt& cnt) {
+  if (!got) {
+    contrib = vmul(thr, v3(S.bg[0], S.bg[1], S.bg[2]));
+    return true;
+  }
+  const DMat m = S.mats[h.mat];
+  if (m.type == RT_MAT_DIFFUSE_LIGHT) {
+    const V3 e = h.ff ? v3(0, 0, 0) : texture_value<F>(S, m.tex, h.u, h.v, h.p);
+    contrib = vmul(thr, e);
+    return true;
+  }
+  Scatter s;
+  if constexpr ((F & F_COUNT) != 0) cnt.light += (m.type == RT_MAT_LAMBERTIAN && S.lights >= 0);
+  scatter<F>(S, m, ray, h, g, s);
+  if (s.specular) {
+    thr = vmul(thr, s.att);
+  } else {
+    const double c = dot(h.n, s.ray.d);
+    const double spdf = c < 0 ? 0 : c / kPi;
+    const double k = spdf / s.pdf;
+    thr = vmul(thr, scale(k, s.att));
+  }
+  ray = s.ray;
+  --depth;
+  return false;
+}
+
+// ---------------------------------------------------------------- tier B: Philox per (pixel, sample)
+// Wave-reduce a per-lane counter and add it once per wave.
+__device__ __forceinline__ void wave_add(unsigned long long* dst, unsigned long long v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off);
+  if ((threadIdx.x & 63) == 0) atomicAdd(dst, v);
+}
+
+// The persistent tier-B loop, shared by the global-memory and LDS-staged kernels.
+template <unsigned F>
+__device__ __forceinline__ void philox_loop(const RenderArgs& A, const Scene& S, int* stk, int stride) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+  long long w = -1;  // the current chunk's slot in A.partial
+  bool done = false, path = false;
+  int px = 0, row = 0, s = 0, s_end = 0, depth = 0;
+  Ray ray;
+  V3 thr = v3(0, 0, 0), sum = v3(0, 0, 0);
+  RngPhilox g;
+  g.init(A.seed, 0, 0);
+  Cnt cnt{};
+  unsigned long long segs = 0, blocks = 0, samples = 0;
+  unsigned long long ph_acq = 0, ph_trav = 0, ph_shade = 0, s0 = 0, s1 = 0, s2 = 0;
+
+  for (;;) {
+    if constexpr ((F & F_COUNT) != 0) s0 = stamp();
+    // acquire pixels for idle lanes: one atomic per wave per round
+    for (;;) {
+      const bool need = (w < 0) && !done;
+      const unsigned long long mask = __ballot(need);
+      if (!mask) break;
+      const int leader = __ffsll((long long)mask) - 1;
+      unsigned long long base = 0;
+      if (lane == leader) base = atomicAdd(A.counter, (unsigned long long)__popcll(mask));
+      base = __shfl(base, leader);
+      if (need) {
+        const long long wi = (long long)(base + __popcll(mask & lanes_below));
+        if (wi >= A.work_total) {
+          done = true;
+        } else if (work_item(A, (uint32_t)wi, px, row, s, s_end, w)) {
+          sum = v3(0, 0, 0);
+          path = false;
+        } else {
+          w = -1;
+        }
+      }
+    }
+    if (w < 0) break;  // no pixel left for this lane (done); the others keep going
+    if (!path) {  // start sample s: uniformRandomUVs' pair, then getRay
+      const uint32_t pid = (uint32_t)((long long)row * A.W + px);
+      g.init(A.seed, pid, (uint32_t)s);
+      g.reserve(3);  // the UV pair and the first disk try
+      const double ru = g.draw(), rv = g.draw();
+      const int y = A.H - 1 - row;
+      const double u = ((double)px + ru) / (double)A.W;
+      const double v = ((double)y + rv) / (double)A.H;
+      ray = get_ray(A.cam, u, v, g);
+      thr = v3(1.0, 1.0, 1.0);
+      depth = A.max_depth;
+      path = true;
+    }
+    V3 contrib;
+    if constexpr ((F & F_COUNT) != 0) {
+      segs += depth > 0;
+      s1 = stamp();
+      s2 = s1;
+    }
+    const bool ended = segment<F>(A, S, ray, thr, depth, g, stk, contrib, cnt, stride, &s2);
+    if constexpr ((F & F_COUNT) != 0) {
+      const unsigned long long s3 = stamp();
+      ph_acq += s1 - s0;
+      ph_trav += s2 - s1;
+      ph_shade += s3 - s2;
+    }
+    if (ended) {
+      if constexpr ((F & F_COUNT) != 0) {
+        blocks += g.pair;
+        ++samples;
+      }
+      if (A.flags & RT_FLAG_NAN_ZERO) contrib = nan_zero(contrib);
+      sum = sum + contrib;
+      path = false;
+      ++s;
+      const bool all_nan = (A.flags & RT_FLAG_NAN_CULL) && sum.x != sum.x && sum.y != sum.y && sum.z != sum.z;
+      if (s == s_end || all_nan) {
+        store_partial(A, w, sum);
+        w = -1;
+      }
+    }
+  }
+  if constexpr ((F & F_COUNT) != 0) {  // lanes re-converge after the loop: one add per wave
+    wave_add(&A.work[0], segs);
+    wave_add(&A.work[1], cnt.box);
+    wave_add(&A.work[2], cnt.prim);
+    wave_add(&A.work[3], cnt.other);
+    wave_add(&A.work[4], cnt.light);
+    wave_add(&A.work[5], blocks);
+    wave_add(&A.work[6], samples);
+    if ((threadIdx.x & 63) == 0) {  // wave-uniform phase times (s_memtime ticks)
+      atomicAdd(&A.work[8], ph_acq);
+      atomicAdd(&A.work[9], ph_trav);
+      atomicAdd(&A.work[10], ph_shade);
+    }
+  }
+}
+
+template <unsigned F, int WAVES>
+__global__ void __launch_bounds__(RT_BLOCK, WAVES) render_philox(RenderArgs A) {
+  __shared__ int stk_mem[RT_STACK * RT_BLOCK];
+  philox_loop<F>(A, A.S, &stk_mem[threadIdx.x], RT_BLOCK);
+}
+
+// LDS-staged variant: one workgroup of WAVES*4 waves per CU; the whole node array is copied
+// into LDS once, ahead of the traversal stack, so every node fetch of the traversal's
+// dependent chain is an LDS read (~64 cycles) instead of an L2 hit (~200-500 cycles).
+template <unsigned F, int WAVES>
+__global__ void __launch_bounds__(WAVES * 256, WAVES) render_philox_lds(RenderArgs A, int n_nodes, int stack_entries) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  rt_node* nodes = reinterpret_cast<rt_node*>(lds);
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(A.S.nodes);
+    uint4* dst = reinterpret_cast<uint4*>(lds);
+    const int n16 = n_nodes * (int)(sizeof(rt_node) / 16);
+    for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  Scene S = A.S;
+  S.nodes = nodes;
+  int* stk = reinterpret_cast<int*>(lds + (size_t)n_nodes * sizeof(rt_node)) + threadIdx.x;
+  (void)stack_entries;
+  philox_loop<F>(A, S, stk, WAVES * 256);
+}
+
+
+// Tier-B loop with ray replacement (media-free worlds without instance frames): traversal state
+// persists in registers across iterations; each iteration first shades the lanes whose walk has
+// ended and starts their next segment (or sample, or pixel), then steps every walking lane one
+// node at a time until at most trav_stop/64 of the live lanes are still walking. Lanes never
+// wait for the slowest walk of their wave, and shading runs for many lanes at once.
+template <unsigned F>
+__device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S, int* stk, int stride, int* side_p,
+                                             volatile uint32_t* wq) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const bool joint = !(A.flags & RT_FLAG_REFERENCE_CULL);
+
+  long long w = -1;  // the current chunk's slot in A.partial
+  bool done = false, walking = false, ready = false;
+  // (worlds walked in the reference's order) the stream position at the start of the walk: a walk
+  // redone for an exact tie repeats its media draws
+  uint32_t walk_mark = 0;
+  // wq[0..1]: the wave's claimed, not yet handed out work-items [next, end), in LDS (lanes that
+  // are walking skip the acquisition code, so a per-lane copy would go stale); indices are < 2^32
+  // (launch_philox checks)
+  if (lane == 0) {
+    wq[0] = 0u;
+    wq[1] = 0u;
+  }
+  int px = 0, row = 0, s = 0, s_end = 0, depth = 0;
+  V3 thr = v3(0, 0, 0), sum = v3(0, 0, 0);
+  RngPhilox g;
+  g.init(A.seed, 0, 0);
+  Trav t;  // the segment's ray lives only here between segments (no second copy is carried)
+  Side side{side_p, stride};
+  Cnt cnt{};
+  unsigned long long segs = 0, blocks = 0, samples = 0, ph_setup = 0, ph_trav = 0, ph_shade = 0;
+
+  // sample s is over: add its colour; the chunk is done after its last sample
+  auto end_sample = [&](V3 contrib) __attribute__((always_inline)) {
+    if constexpr ((F & F_COUNT) != 0) {
+      blocks += g.pair;
+      ++samples;
+    }
+    if (A.flags & RT_FLAG_NAN_ZERO) contrib = nan_zero(contrib);
+    sum = sum + contrib;
+    ++s;
+    const bool all_nan = (A.flags & RT_FLAG_NAN_CULL) && sum.x != sum.x && sum.y != sum.y && sum.z != sum.z;
+    if (s == s_end || all_nan) {
+      store_partial(A, w, sum);
+      w = -1;
+    }
+  };
+
+  for (;;) {
+    unsigned long long s0 = 0;
+    if constexpr ((F & F_COUNT) != 0) {
+      s0 = stamp();
+      ++cnt.oslot;
+    }
+    // ---- shade finished walks, then set up the next walk for every lane that is not walking
+    if (ready && t.tie && !t.redo) {  // exact tie: redo this walk as the reference does (once)
+      ready = false;
+      if constexpr ((F & F_COUNT) != 0) ++cnt.ties;
+      if constexpr (kRefMixed<F>) g.rewind(walk_mark);  // (the walk's media draws repeat)
+      trav_restart_ref(t, S.world_ref, INFINITY, true);
+      walking = true;
+    }
+    // the next walk's ray: a scattered ray (next segment) or a camera ray (next sample), parked in
+    // t.ray (free once the walk's hit is recorded); both kinds of lane start their walk together
+    // below, so the walk set-up runs once per wave
+    bool start = false;
+    if (ready) {
+      ready = false;
+      Hit h;
+      Ray ray = plain(t.ray);  // (every frame has closed: the world ray again)
+      const bool got = trav_finish<F>(S, t, ray, kEps, h, side);
+      V3 contrib;
+      if (shade_hit<F>(S, got, h, ray, thr, depth, g, contrib, cnt)) {
+        end_sample(contrib);
+      } else if (depth <= 0) {  // rayColor's d <= 0 -> black (thr * 0 keeps a NaN throughput NaN)
+        end_sample(vmul(thr, v3(0.0, 0.0, 0.0)));
+      } else {  // next segment of the same path
+        t.ray.o = ray.o;
+        t.ray.d = ray.d;
+        t.ray.tm = ray.tm;
+        start = true;
+        if constexpr ((F & F_COUNT) != 0) ++segs;
+      }
+    }
+    unsigned long long s0b = 0;
+    if constexpr ((F & F_COUNT) != 0) s0b = stamp();
+    while (!walking && !start) {
+      // acquire work-items for idle lanes: from the wave's claimed range first; when it runs short,
+      // one atomic claims a batch of A.batch more (exactly the lanes' need once the counter is near
+      // the end, so that no wave hoards the frame's last items)
+      for (;;) {
+        const bool need = (w < 0) && !done;
+        const unsigned long long mask = __ballot(need);
+        if (!mask) break;
+        const uint32_t n_need = (uint32_t)__popcll(mask);
+        const uint32_t q_next = wq[0], q_end = wq[1];
+        const uint32_t avail = q_end - q_next;
+        uint32_t base2 = q_next, end2 = q_end;  // items past `avail` come from a new claim
+        if (avail < n_need) {
+          const int leader = __ffsll((long long)mask) - 1;
+          unsigned long long claim = 0;
+          if (lane == leader) {
+            // batch: A.batch items, fewer as the frame runs out (the wave's last claim end tells it
+            // roughly how many remain), so that no wave hoards the tail; never less than the need
+            const uint32_t want = n_need - avail;
+            const long long rem = A.work_total - (long long)q_end;
+            const uint32_t b = rem <= 0 ? 0u : (uint32_t)fminf((float)A.batch, (float)rem * A.batch_per_item);
+            const uint32_t got = want < b ? b : want;
+            const unsigned long long c0 = atomicAdd(A.counter, (unsigned long long)got);
+            // (claims past 2^32 only happen once every item is handed out: clamp, the lanes see
+            // `done`); the claim and its size travel together in one broadcast
+            claim = (c0 < 0xffff0000ull ? c0 : 0xffff0000ull) | ((unsigned long long)got << 32);
+          }
+          const unsigned long long c1 = __shfl(claim, leader);
+          base2 = (uint32_t)c1;
+          end2 = base2 + (uint32_t)(c1 >> 32);
+        }
+        const uint32_t rank = (uint32_t)__popcll(mask & lanes_below);
+        if (need) {
+          const long long wi = (long long)(rank < avail ? q_next + rank : base2 + (rank - avail));
+          if (wi >= A.work_total) {
+            done = true;
+          } else if (work_item(A, (uint32_t)wi, px, row, s, s_end, w)) {
+            sum = v3(0, 0, 0);
+          } else {
+            w = -1;
+          }
+        }
+        const int leader = __ffsll((long long)mask) - 1;
+        if (lane == leader) {
+          wq[0] = avail < n_need ? base2 + (n_need - avail) : q_next + n_need;
+          wq[1] = end2;
+        }
+      }
+      if (w < 0) break;  // no work left for this lane
+      // start sample s: uniformRandomUVs' pair, then getRay
+      const uint32_t pid = (uint32_t)((long long)row * A.W + px);
+      g.init(A.seed, pid, (uint32_t)s);
+      g.reserve(3);  // the UV pair and the first disk try
+      const double ru = g.draw(), rv = g.draw();
+      const int y = A.H - 1 - row;
+      const double u = ((double)px + ru) / (double)A.W;
+      const double v = ((double)y + rv) / (double)A.H;
+      const Ray cray = get_ray(A.cam, u, v, g);
+      t.ray.o = cray.o;
+      t.ray.d = cray.d;
+      t.ray.tm = cray.tm;
+      thr = v3(1.0, 1.0, 1.0);
+      depth = A.max_depth;
+      if (depth <= 0) {
+        end_sample(vmul(thr, v3(0.0, 0.0, 0.0)));
+        continue;
+      }
+      start = true;
+      if constexpr ((F & F_COUNT) != 0) ++segs;
+    }
+    if (start) {
+      trav_begin<F>(t, plain(t.ray), S.world, kEps, INFINITY);
+      // worlds with media or frames: the reference's order over the re-bounded skeleton
+      if (S.ref_walk) trav_restart_ref(t, S.world, INFINITY);
+      if constexpr (kRefMixed<F>) walk_mark = g.consumed();
+      // (media draw inside the walk: top the FIFO up here, where the starting lanes run together,
+      // so that a medium's draw does not evaluate Philox inside a divergent walk step; the words and
+      // their order are the stream's, and consumed() is unchanged)
+      if constexpr ((F & F_MEDIA) != 0) g.reserve(2);
+      walking = true;
+    }
+    if (!walking) break;  // this lane is finished; the rest of the wave carries on without it
+    unsigned long long s1 = 0;
+    if constexpr ((F & F_COUNT) != 0) s1 = stamp();
+    // ---- walk until few lanes are still walking
+    const int live = __popcll(__ballot(true));
+    const int stop = (live * A.trav_stop) >> 6;
+    const int ls = (F & F_WIDE) ? A.leaf_stop : A.box_first;
+    walk_until<F>(S, t, walking, kEps, stk, stride, joint, stop, (live * ls) >> 6, cnt, g, side);
+    ready = !walking;
+    if constexpr ((F & F_COUNT) != 0) {
+      const unsigned long long s2 = stamp();
+      ph_shade += s0b - s0;
+      ph_setup += s1 - s0b;
+      ph_trav += s2 - s1;
+    }
+  }
+  if constexpr ((F & F_COUNT) != 0) {
+    wave_add(&A.work[0], segs);
+    wave_add(&A.work[1], cnt.box);
+    wave_add(&A.work[2], cnt.prim);
+    wave_add(&A.work[3], cnt.other);
+    wave_add(&A.work[4], cnt.light);
+    wave_add(&A.work[5], blocks);
+    wave_add(&A.work[6], samples);
+    wave_add(&A.work[7], cnt.wide);
+    wave_add(&A.work[11], cnt.islot);
+    wave_add(&A.work[12], cnt.lslot);
+    wave_add(&A.work[13], cnt.oslot);
+    wave_add(&A.work[14], cnt.phit);
+    wave_add(&A.work[15], cnt.ties);
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(&A.work[8], ph_setup);
+      atomicAdd(&A.work[9], ph_trav);
+      atomicAdd(&A.work[10], ph_shade);
+    }
+  }
+}
+
+// LDS ints per lane of a kernel: the traversal stack, then (instance frames possible) Side slots
+template <unsigned F>
+constexpr int lane_ints() {
+  return ((F & F_WIDE) ? RT_WSTACK : RT_STACK) + ((F & F_FRAMES) ? kSideInts : 0);
+}
+
+// Global-memory replacement loop: the lane stacks (and Side slots) in dynamic LDS sized by the host
+// for the world's stack bound (`stack_entries` per lane), not for the RT_STACK / RT_WSTACK maxima:
+// the LDS per workgroup then does not cap the occupancy (C4: 54 -> 40 ints per lane, 2.5 -> 3 waves
+// per SIMD).
+template <unsigned F, int WAVES>
+__global__ void __launch_bounds__(RT_BLOCK, WAVES) render_philox2(RenderArgs A, int stack_entries) {
+  extern __shared__ __attribute__((aligned(16))) int stk_mem[];
+  __shared__ uint32_t wave_q[RT_BLOCK / 64][2];
+  philox_loop2<F>(A, A.S, &stk_mem[threadIdx.x], RT_BLOCK, &stk_mem[stack_entries * RT_BLOCK + threadIdx.x],
+                  wave_q[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)]);
+}
+
+// LDS-staged replacement loop: the traversal's node array (the wide records for F_WIDE, else the
+// flat nodes) and the per-lane stacks live in the CU's LDS; leaves are read from global memory
+// under F_WIDE.
+// LEAF_LDS: the 4-wide walk's leaf table is staged too (n_leaves > 0); as its own instantiation,
+// so that the leaf reads compile to ds_read (a pointer that is LDS or global at run time would
+// make them flat loads, which wait on both the vector-memory and LDS counters).
+template <unsigned F, int WAVES, bool LEAF_LDS = false>
+__global__ void __launch_bounds__(WAVES * 256, WAVES)
+    render_philox2_lds(RenderArgs A, int n_nodes, int stack_entries, int n_leaves) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  __shared__ uint32_t wave_q[WAVES * 4][2];  // (static: kStaticLds bytes ahead of the dynamic LDS)
+  constexpr int rec = (F & F_WIDE) ? (int)sizeof(rt_wnode) : (int)sizeof(rt_node);
+  {
+    const uint4* src = (F & F_WIDE) ? reinterpret_cast<const uint4*>(A.S.wnodes)
+                                    : reinterpret_cast<const uint4*>(A.S.nodes);
+    uint4* dst = reinterpret_cast<uint4*>(lds);
+    const int n16 = n_nodes * (rec / 16);
+    for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+    // F_WIDE: the leaf table too, when it fits (n_leaves > 0)
+    const uint4* lsrc = reinterpret_cast<const uint4*>(A.S.leaves);
+    uint4* ldst = reinterpret_cast<uint4*>(lds + (size_t)n_nodes * rec);
+    const int l16 = n_leaves * (int)(sizeof(rt_node) / 16);
+    for (int i = threadIdx.x; i < l16; i += blockDim.x) ldst[i] = lsrc[i];
+  }
+  __syncthreads();
+  Scene S = A.S;
+  if constexpr ((F & F_WIDE) != 0) S.wnodes = reinterpret_cast<const rt_wnode*>(lds);
+  else S.nodes = reinterpret_cast<const rt_node*>(lds);
+  if constexpr (LEAF_LDS) S.leaves = reinterpret_cast<const rt_node*>(lds + (size_t)n_nodes * rec);
+  else n_leaves = 0;
+  int* stk = reinterpret_cast<int*>(lds + (size_t)n_nodes * rec + (size_t)n_leaves * sizeof(rt_node)) + threadIdx.x;
+  // (the host sizes the dynamic LDS for stack_entries stack ints + kSideInts Side ints per lane
+  // when F has F_FRAMES)
+  philox_loop2<F>(A, S, stk, WAVES * 256, stk + stack_entries * WAVES * 256,
+                  wave_q[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)]);
+}
+
+// Tier B: a slab pixel's chunk sums added in chunk order, then averaged and stored (rt.h).
+__global__ void __launch_bounds__(256) combine_chunks(RenderArgs A) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= A.slab) return;
+  int px, row;
+  if (!work_pixel(A, (uint32_t)idx, px, row)) return;  // outside the image: never assembled
+  V3 acc = v3(0, 0, 0);
+  for (int k = 0; k < A.chunks; ++k) {
+    const double* q = A.partial + ((long long)k * A.slab + idx) * 3;
+    acc = acc + v3(q[0], q[1], q[2]);
+  }
+  store_pixel(A, idx, divide(acc, (double)A.spp));
+}
+
+// ---------------------------------------------------------------- tier A: the reference's stream
+// One lane per image column; rows top to bottom; each pixel draws its 2*ns UVs first and uses
+// them in reverse draw order (uniformRandomUVs' foldr, Lib.hs:1358-1371) — the UV pairs are
+// recomputed from the pixel's starting state (SplitMix is seed + k*gamma), no list is stored.
+template <unsigned F>
+__global__ void __launch_bounds__(RT_BLOCK) render_exact(RenderArgs A) {
+  __shared__ int stk_mem[RT_STACK * RT_BLOCK];
+  int* stk = &stk_mem[threadIdx.x];
+  // Tier A reproduces the reference's stream exactly, exact ties included: walk the caller's tree.
+  Scene S = A.S;
+  S.world = S.world_ref;
+  const int x = blockIdx.x * RT_BLOCK + threadIdx.x;
+  if (x >= A.W) return;
+  RngExact g{A.gens[2 * x], A.gens[2 * x + 1]};
+  const int ns = A.spp;
+  for (int row = 0; row < A.H; ++row) {
+    const int y = A.H - 1 - row;
+    const uint64_t seed0 = g.seed;
+    g.seed += (uint64_t)(2 * (long long)ns) * g.gamma;
+    V3 sum = v3(0, 0, 0);
+    for (int j = 0; j < ns; ++j) {
+      const int i = ns - 1 - j;
+      const double ru = word_to_draw(mix64(seed0 + (uint64_t)(2 * i + 1) * g.gamma));
+      const double rv = word_to_draw(mix64(seed0 + (uint64_t)(2 * i + 2) * g.gamma));
+      const double u = ((double)x + ru) / (double)A.W;
+      const double v = ((double)y + rv) / (double)A.H;
+      Ray ray = get_ray(A.cam, u, v, g);
+      V3 thr = v3(1.0, 1.0, 1.0), contrib;
+      int depth = A.max_depth;
+      Cnt cnt{};
+      while (!segment<F>(A, S, ray, thr, depth, g, stk, contrib, cnt)) {
+      }
+      sum = sum + contrib;
+    }
+    store_pixel(A, (long long)row * A.W + x, divide(sum, (double)ns));
+  }
+  A.gens[2 * x] = g.seed;
+}
+
+// ---------------------------------------------------------------- slab -> image
+template <class T>
+__global__ void assemble(const T* slabs, T* image, int W, int H, int tile, int tiles_x, int shards,
+                         long long slab_pixels) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)W * H) return;
+  const int row = (int)(i / W), px = (int)(i % W);
+  const int gt = (row / tile) * tiles_x + (px / tile);
+  const int shard = gt % shards;
+  const long long lt = gt / shards;
+  const int bpr = tile >> 3;
+  const int bx = (px % tile) >> 3, by = (row % tile) >> 3;
+  const int within = (by * bpr + bx) * 64 + (row & 7) * 8 + (px & 7);
+  const long long src = (long long)shard * slab_pixels + lt * tile * tile + within;
+  image[i * 3 + 0] = slabs[src * 3 + 0];
+  image[i * 3 + 1] = slabs[src * 3 + 1];
+  image[i * 3 + 2] = slabs[src * 3 + 2];
+}
+
+// ---------------------------------------------------------------- debug: closest hits
+template <unsigned F>
+__global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* rays, int n, double tmin,
+                                                         double tmax, uint64_t seed, int joint, int walk, double* out) {
+  __shared__ int stk_mem[lane_ints<F>() * RT_BLOCK];
+  int* stk = &stk_mem[threadIdx.x];
+  Side side{&stk_mem[((F & F_WIDE) ? RT_WSTACK : RT_STACK) * RT_BLOCK + threadIdx.x], RT_BLOCK};
+  const int i = blockIdx.x * RT_BLOCK + threadIdx.x;
+  if (i >= n) return;
+  const double* q = rays + 7 * (long long)i;
+  const Ray r{v3(q[0], q[1], q[2]), v3(q[3], q[4], q[5]), q[6]};
+  RngPhilox g;
+  g.init(seed, (uint32_t)i, 0);
+  Hit h;
+  double* o = out + 12 * (long long)i;
+  Cnt cnt{};
+  bool got;
+  if (walk == 0) {
+    got = traverse<F>(S, S.ref_walk ? S.world_ref : S.world, r, tmin, tmax, h, g, stk, joint != 0, cnt);
+  } else {  // the render loop's resumable walk (binary, or 4-wide under F_WIDE)
+    Trav t;
+    trav_begin<F>(t, r, S.world, tmin, tmax);
+    if (S.ref_walk) trav_restart_ref(t, S.world, tmax);  // (the re-bounded skeleton, mixed walk)
+    bool walking = true;
+    walk_until<F>(S, t, walking, tmin, stk, RT_BLOCK, joint != 0, 0, 0, cnt, g, side);
+    if (t.tie) {
+      if (S.ref_walk) g.rewind(0);  // media draws repeat on the caller's tree
+      trav_restart_ref(t, S.world_ref, tmax, true);
+      while (trav_step<F>(S, t, tmin, stk, RT_BLOCK, joint != 0, cnt, g, side)) {
+      }
+    }
+    got = trav_finish<F>(S, t, r, tmin, h, side);
+  }
+  if (got) {
+    o[0] = 1; o[1] = h.t;
+    o[2] = h.p.x; o[3] = h.p.y; o[4] = h.p.z;
+    o[5] = h.n.x; o[6] = h.n.y; o[7] = h.n.z;
+    o[8] = h.u; o[9] = h.v; o[10] = h.ff; o[11] = h.mat;
+  } else {
+    for (int k = 0; k < 12; ++k) o[k] = 0;
+  }
+}
+
+// ---------------------------------------------------------------- debug: per-function probes
+// The hot-path functions one at a time on device inputs (rt_debug_probe; layouts in rt.h and
+// oracle/oracle.c oracle_probe): record i draws from its own tier-B Philox stream (key = seed, pid = i,
+// sample 0), so the oracle's golden vectors consume the same numbers.
+constexpr int kProbeIn[5] = {18, 3, 6, 6, 2}, kProbeOut[5] = {14, 4, 2, 3, 8};
+template <unsigned F>
+__global__ void __launch_bounds__(RT_BLOCK) fn_probe(Scene S, rt_camera cam, int op, const double* in, int n,
+                                                    uint64_t seed, double* out) {
+  const int i = blockIdx.x * RT_BLOCK + threadIdx.x;
+  if (i >= n) return;
+  const double* q = in + (long long)kProbeIn[op] * i;
+  double* o = out + (long long)kProbeOut[op] * i;
+  for (int k = 0; k < kProbeOut[op]; ++k) o[k] = 0.0;
+  RngPhilox g;
+  g.init(seed, (uint32_t)i, 0);
+  if (op == 0) {  // scatter (or emitted for DiffuseLight), as shade_hit runs it
+    const Ray r{v3(q[0], q[1], q[2]), v3(q[3], q[4], q[5]), q[6]};
+    Hit h;
+    h.t = q[7];
+    h.p = v3(q[8], q[9], q[10]);
+    h.n = v3(q[11], q[12], q[13]);
+    h.u = q[14];
+    h.v = q[15];
+    h.ff = (int)q[16];
+    h.mat = (int)q[17];
+    const DMat m = S.mats[h.mat];
+    if (m.type == RT_MAT_DIFFUSE_LIGHT) {
+      const V3 e = h.ff ? v3(0, 0, 0) : texture_value<F>(S, m.tex, h.u, h.v, h.p);
+      o[8] = e.x, o[9] = e.y, o[10] = e.z;
+    } else {
+      Scatter sc;
+      scatter<F>(S, m, r, h, g, sc);
+      o[0] = 1;
+      o[1] = sc.ray.o.x, o[2] = sc.ray.o.y, o[3] = sc.ray.o.z;
+      o[4] = sc.ray.d.x, o[5] = sc.ray.d.y, o[6] = sc.ray.d.z, o[7] = sc.ray.tm;
+      o[8] = sc.att.x, o[9] = sc.att.y, o[10] = sc.att.z;
+      o[11] = sc.pdf;
+      o[12] = sc.specular;
+    }
+    o[13] = g.consumed();
+  } else if (op == 1) {  // htblRandom on the lights tree
+    const V3 d = htbl_random(S, S.lights, v3(q[0], q[1], q[2]), g);
+    o[0] = d.x, o[1] = d.y, o[2] = d.z;
+    o[3] = g.consumed();
+  } else if (op == 2) {  // htblPdfValue on the lights tree
+    const V3 org = v3(q[0], q[1], q[2]), v = v3(q[3], q[4], q[5]);
+    o[0] = S.lights < 0 ? 0.0 : htbl_pdf_value<F, RT_LIGHT_DEPTH>(S, S.lights, org, v, prep(Ray{org, v, 0.0}));
+    o[1] = g.consumed();
+  } else if (op == 3) {  // textureValue
+    const V3 a = texture_value<F>(S, (int)q[0], q[1], q[2], v3(q[3], q[4], q[5]));
+    o[0] = a.x, o[1] = a.y, o[2] = a.z;
+  } else {  // getRay
+    const Ray r = get_ray(cam, q[0], q[1], g);
+    o[0] = r.o.x, o[1] = r.o.y, o[2] = r.o.z;
+    o[3] = r.d.x, o[4] = r.d.y, o[5] = r.d.z, o[6] = r.tm;
+    o[7] = g.consumed();
+  }
+}
+
+// ---------------------------------------------------------------- debug: numerics probe
+__global__ void math_probe(int op, const double* x, const double* y, int n, double* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double a = x[i], b = y[i];
+  double r;
+  switch (op) {
+    case 0: r = a / b; break;
+    case 1: r = div_exact(a, b, 1.0 / b); break;
+    case 2: r = sqrt(a); break;
+    case 3: r = sin(a); break;
+    case 4: r = cos(a); break;
+    case 5: r = atan(a); break;
+    case 6: r = asin(a); break;
+    case 7: r = log(a); break;
+    case 8: r = pow(a, b); break;
+    case 9: r = ghc_atan2(a, b); break;
+    case 11: r = pow5(a); break;
+    default: r = tan(a); break;
+  }
+  out[i] = r;
+}
+
+
+// Kernel variants: spheres-only (configs 1, 2, 5), Cornell-like (rects, instances, lights), full.
+constexpr unsigned kVarSpheres = 0u;
+constexpr unsigned kVarCornell = F_RECT | F_INST | F_LIGHTS;
+// the full variant without light sampling (lights Unhittable: next_week_final, the textured
+// scenes), whose Lambertian scatter needs no lights-tree code
+constexpr unsigned kVarFullDark = F_ALL & ~F_LIGHTS;
+unsigned variant_for(unsigned f) {
+  if ((f & ~kVarSpheres) == 0) return kVarSpheres;
+  if ((f & ~kVarCornell) == 0) return kVarCornell;
+  return (f & F_LIGHTS) ? F_ALL : kVarFullDark;
+}
+bool is_full(unsigned var) { return (var & F_FRAMES) != 0; }
+
+// Kernel pointer for (variant, loop, LDS-staged?, waves per SIMD, counting build?); loop 0 = one
+// sample per lane walk, 1 = ray replacement over the binary tree, 2 = replacement over the
+// 4-wide tree.
+template <unsigned V>
+const void* pick_w(bool lds, int w, bool leaf_lds = false) {
+  if constexpr ((V & F_WIDE) != 0) {
+    if (lds && leaf_lds) {
+      if (w == 4) return (const void*)render_philox2_lds<V, 4, true>;
+      if (w == 2) return (const void*)render_philox2_lds<V, 2, true>;
+      if (w == 3) return (const void*)render_philox2_lds<V, 3, true>;
+    }  // (1 wave: the leaves are read from global memory)
+  }
+  if (lds) {
+    if (w == 2) return (const void*)render_philox2_lds<V, 2>;
+    if (w == 4) return (const void*)render_philox2_lds<V, 4>;
+    if (w == 1) return (const void*)render_philox2_lds<V, 1>;
+    return (const void*)render_philox2_lds<V, 3>;
+  }
+  if (w == 2) return (const void*)render_philox2<V, 2>;
+  if (w == 3) return (const void*)render_philox2<V, 3>;
+  if (w == 4) return (const void*)render_philox2<V, 4>;
+  return (const void*)render_philox2<V, 1>;
+}
+template <unsigned V>
+const void* pick(int loop, bool lds, int w, bool count, bool leaf_lds) {
+  if (count) {
+    if (loop == 2) return (const void*)render_philox2<V | F_WIDE | F_COUNT, 1>;
+    return loop ? (const void*)render_philox2<V | F_COUNT, 1> : (const void*)render_philox<V | F_COUNT, 1>;
+  }
+  if (loop == 2) return pick_w<V | F_WIDE>(lds, w, leaf_lds);
+  if (loop == 1) return pick_w<V>(lds, w);
+  if (lds) {
+    if (w == 2) return (const void*)render_philox_lds<V, 2>;
+    if (w == 4) return (const void*)render_philox_lds<V, 4>;
+    if (w == 1) return (const void*)render_philox_lds<V, 1>;
+    return (const void*)render_philox_lds<V, 3>;
+  }
+  if (w == 2) return (const void*)render_philox<V, 2>;
+  if (w == 3) return (const void*)render_philox<V, 3>;
+  if (w == 4) return (const void*)render_philox<V, 4>;
+  return (const void*)render_philox<V, 1>;
+}
+// full variants (media, frames, textures, motion): ray replacement over the caller's tree in the
+// reference's order (loop 1), or the per-sample loop (loop 0)
+template <unsigned V>
+const void* pick_full(int loop, bool lds, int w, bool count) {
+  if (count) return loop ? (const void*)render_philox2<V | F_COUNT, 1> : (const void*)render_philox<V | F_COUNT, 1>;
+  if (loop) {
+    if (lds) return w >= 3 ? (const void*)render_philox2_lds<V, 3> : (const void*)render_philox2_lds<V, 2>;
+    return w >= 3 ? (const void*)render_philox2<V, 3> : (const void*)render_philox2<V, 2>;
+  }
+  return w >= 2 ? (const void*)render_philox<V, 2> : (const void*)render_philox<V, 1>;
+}
+
+}  // namespace
+
+// Render-kernel tables, one per kernel translation unit: the kernel for (loop, LDS-staged?, waves per
+// SIMD, counting build?, leaf table in LDS?) of that unit's variant(s).
+namespace rt {
+const void* philox_kernel_spheres(int loop, bool lds, int w, bool count, bool leaf_lds);
+const void* philox_kernel_cornell(int loop, bool lds, int w, bool count, bool leaf_lds);
+const void* philox_kernel_full(int loop, bool lds, int w, bool count);
+const void* philox_kernel_full_dark(int loop, bool lds, int w, bool count);
+}  // namespace rt

@@ -1,6 +1,8 @@
-"""Per-kernel register / scratch / occupancy table of rt_render.hip (hipcc -Rpass-analysis).
+"""Per-kernel register / scratch / occupancy table of the render kernels (hipcc -Rpass-analysis).
 
-    python scripts/resources.py [filter] [-- extra hipcc flags]
+    python scripts/resources.py [filter] [--tu spheres|cornell|full|full_dark|render ...] [-- extra hipcc flags]
+
+The translation units (rt_k_*.hip, rt_render.hip) compile in parallel; --tu limits the run to some.
 """
 import re
 import subprocess
@@ -15,11 +17,22 @@ def main():
     if "--" in args:
         i = args.index("--")
         args, extra = args[:i], args[i + 1:]
+    tus = ["spheres", "cornell", "full", "full_dark", "render"]
+    if "--tu" in args:
+        i = args.index("--tu")
+        sel = [a for a in args[i + 1:] if a in tus]
+        args = args[:i] + [a for a in args[i + 1:] if a not in tus]
+        tus = sel
     filt = args[0] if args else ""
-    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
-           "-fno-fast-math", f"-I{ROOT}/include", "-c", f"{ROOT}/ray-tracing_amd/csrc/rt_render.hip", "-o",
-           "/dev/null", "-Rpass-analysis=kernel-resource-usage"] + extra
-    out = subprocess.run(cmd, capture_output=True, text=True).stderr
+    csrc = f"{ROOT}/ray-tracing_amd/csrc"
+    procs = []
+    for tu in tus:
+        src = f"{csrc}/rt_render.hip" if tu == "render" else f"{csrc}/rt_k_{tu}.hip"
+        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+               "-fno-fast-math", f"-I{ROOT}/include", "-c", src, "-o", "/dev/null",
+               "-Rpass-analysis=kernel-resource-usage"] + extra
+        procs.append(subprocess.Popen(cmd, stderr=subprocess.PIPE, stdout=subprocess.DEVNULL, text=True))
+    out = "\n".join(p.communicate()[1] for p in procs)
     rows, cur = [], None
     for line in out.splitlines():
         m = re.search(r"remark: +([A-Za-z][\w \[\]/]*?): (.*?) \[-Rpass", line)
