@@ -23,6 +23,11 @@
 #define RT_LIGHT_DEPTH 2  /* max BVH depth of the lights tree (host-validated) */
 #define RT_MAX_FRAMES 4   /* max nesting of instance frames on the replacement loop (host-validated) */
 #define RT_FRAME 0x40000000 /* stack-entry tag: instance frame marker */
+#define RT_WNODE 0x10000000 /* node-id tag (mixed walks, F_MIXW): a 4-wide node of a re-bounded subtree */
+#define RT_ISBOX 0x08000000 /* node-id tag: a BVH node (set by the upload on the device copy's BVH children
+                               and on the roots), so that a walk schedules box steps without a load */
+#define RT_WROOT 0x20000000 /* rt_node.c flag of an RT_BVH_ORDERED node whose subtree has a 4-wide tree, */
+#define RT_WROOT_MASK 0x3ffffff /* whose root index is (c >> 2) & RT_WROOT_MASK (mixed walks) */
 #define RT_SUB 0x20000000   /* node-id tag (walks in the reference's order): inside a re-bounded,
                                media-free subtree (below an RT_BVH_ORDERED node) */
 #define RT_CHAIN_PRIM 0x100 /* device node type flag: Translate/Rotate chain ending in a primitive */

@@ -4,5 +4,5 @@
 #include "rt_kernels.h"
 
 namespace rt {
-const void* philox_kernel_full(int loop, bool lds, int w, bool count) { return pick_full<F_ALL>(loop, lds, w, count); }
+const void* philox_kernel_full(int loop, bool lds, int w, bool count) { return pick_full<kVarFull>(loop, lds, w, count); }
 }  // namespace rt

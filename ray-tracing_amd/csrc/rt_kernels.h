@@ -174,14 +174,14 @@ __device__ __forceinline__ bool segment(const RenderArgs& A, const Scene& S, Ray
     return true;
   }
   const DMat m = S.mats[h.mat];
+  const V3 tx = hit_texture<F>(S, m, h);
   if (m.type == RT_MAT_DIFFUSE_LIGHT) {  // scatter -> Nothing: emitted (Lib.hs:880-885)
-    const V3 e = h.ff ? v3(0, 0, 0) : texture_value<F>(S, m.tex, h.u, h.v, h.p);
-    contrib = vmul(thr, e);
+    contrib = vmul(thr, h.ff ? v3(0, 0, 0) : mat_texture<F>(S, m, h, tx));
     return true;
   }
   Scatter s;
   if constexpr ((F & F_COUNT) != 0) cnt.light += (m.type == RT_MAT_LAMBERTIAN && S.lights >= 0);
-  scatter<F>(S, m, ray, h, g, s);
+  scatter<F>(S, m, ray, h, g, s, tx);
   if (s.specular) {
     thr = vmul(thr, s.att);
   } else {
@@ -205,14 +205,14 @@ __device__ __forceinline__ bool shade_hit(const Scene& S, bool got, const Hit& h
     return true;
   }
   const DMat m = S.mats[h.mat];
+  const V3 tx = hit_texture<F>(S, m, h);  // (the kernel's one copy of the texture code)
   if (m.type == RT_MAT_DIFFUSE_LIGHT) {
-    const V3 e = h.ff ? v3(0, 0, 0) : texture_value<F>(S, m.tex, h.u, h.v, h.p);
-    contrib = vmul(thr, e);
+    contrib = vmul(thr, h.ff ? v3(0, 0, 0) : mat_texture<F>(S, m, h, tx));
     return true;
   }
   Scatter s;
   if constexpr ((F & F_COUNT) != 0) cnt.light += (m.type == RT_MAT_LAMBERTIAN && S.lights >= 0);
-  scatter<F>(S, m, ray, h, g, s);
+  scatter<F>(S, m, ray, h, g, s, tx);
   if (s.specular) {
     thr = vmul(thr, s.att);
   } else {
@@ -569,7 +569,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
 // LDS ints per lane of a kernel: the traversal stack, then (instance frames possible) Side slots
 template <unsigned F>
 constexpr int lane_ints() {
-  return ((F & F_WIDE) ? RT_WSTACK : RT_STACK) + ((F & F_FRAMES) ? kSideInts : 0);
+  return ((F & (F_WIDE | F_MIXW)) ? RT_WSTACK : RT_STACK) + ((F & F_FRAMES) ? kSideInts : 0);
 }
 
 // Global-memory replacement loop: the lane stacks (and Side slots) in dynamic LDS sized by the host
@@ -699,7 +699,7 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
                                                          double tmax, uint64_t seed, int joint, int walk, double* out) {
   __shared__ int stk_mem[lane_ints<F>() * RT_BLOCK];
   int* stk = &stk_mem[threadIdx.x];
-  Side side{&stk_mem[((F & F_WIDE) ? RT_WSTACK : RT_STACK) * RT_BLOCK + threadIdx.x], RT_BLOCK};
+  Side side{&stk_mem[((F & (F_WIDE | F_MIXW)) ? RT_WSTACK : RT_STACK) * RT_BLOCK + threadIdx.x], RT_BLOCK};
   const int i = blockIdx.x * RT_BLOCK + threadIdx.x;
   if (i >= n) return;
   const double* q = rays + 7 * (long long)i;
@@ -762,12 +762,13 @@ __global__ void __launch_bounds__(RT_BLOCK) fn_probe(Scene S, rt_camera cam, int
     h.ff = (int)q[16];
     h.mat = (int)q[17];
     const DMat m = S.mats[h.mat];
+    const V3 tx = hit_texture<F>(S, m, h);
     if (m.type == RT_MAT_DIFFUSE_LIGHT) {
-      const V3 e = h.ff ? v3(0, 0, 0) : texture_value<F>(S, m.tex, h.u, h.v, h.p);
+      const V3 e = h.ff ? v3(0, 0, 0) : mat_texture<F>(S, m, h, tx);
       o[8] = e.x, o[9] = e.y, o[10] = e.z;
     } else {
       Scatter sc;
-      scatter<F>(S, m, r, h, g, sc);
+      scatter<F>(S, m, r, h, g, sc, tx);
       o[0] = 1;
       o[1] = sc.ray.o.x, o[2] = sc.ray.o.y, o[3] = sc.ray.o.z;
       o[4] = sc.ray.d.x, o[5] = sc.ray.d.y, o[6] = sc.ray.d.z, o[7] = sc.ray.tm;
@@ -824,11 +825,13 @@ constexpr unsigned kVarSpheres = 0u;
 constexpr unsigned kVarCornell = F_RECT | F_INST | F_LIGHTS;
 // the full variant without light sampling (lights Unhittable: next_week_final, the textured
 // scenes), whose Lambertian scatter needs no lights-tree code
-constexpr unsigned kVarFullDark = F_ALL & ~F_LIGHTS;
+constexpr unsigned kVarFullDark = (F_ALL & ~F_LIGHTS) | F_MIXW;
+// the full variant with light sampling
+constexpr unsigned kVarFull = F_ALL | F_MIXW;
 unsigned variant_for(unsigned f) {
   if ((f & ~kVarSpheres) == 0) return kVarSpheres;
   if ((f & ~kVarCornell) == 0) return kVarCornell;
-  return (f & F_LIGHTS) ? F_ALL : kVarFullDark;
+  return (f & F_LIGHTS) ? kVarFull : kVarFullDark;
 }
 bool is_full(unsigned var) { return (var & F_FRAMES) != 0; }
 
@@ -881,6 +884,7 @@ const void* pick_full(int loop, bool lds, int w, bool count) {
   if (count) return loop ? (const void*)render_philox2<V | F_COUNT, 1> : (const void*)render_philox<V | F_COUNT, 1>;
   if (loop) {
     if (lds) return w >= 3 ? (const void*)render_philox2_lds<V, 3> : (const void*)render_philox2_lds<V, 2>;
+    if (w >= 4) return (const void*)render_philox2<V, 4>;  // (RTAMD_WAVES=4: A/B only)
     return w >= 3 ? (const void*)render_philox2<V, 3> : (const void*)render_philox2<V, 2>;
   }
   return w >= 2 ? (const void*)render_philox<V, 2> : (const void*)render_philox<V, 1>;

@@ -19,6 +19,8 @@
 //    (the reference's per-column SplitMix stream) runs one lane per column.
 #include "rt_kernels.h"
 
+#include <functional>
+
 namespace rt {
 int rebuild_world_bvh(std::vector<rt_node>& nodes, int root);
 int rebuild_for_device(std::vector<rt_node>& nodes, int root);
@@ -53,6 +55,7 @@ struct rt_ctx {
   int n_wnodes = 0;
   int wide_stack_need = 0;
   bool rebuilt_bvh = false;
+  bool mixed_wide = false;   // media / frame world with 4-wide trees over its re-bounded subtrees (F_MIXW)
   bool replace_ok = false;  // frames nest <= RT_MAX_FRAMES deep: the replacement loop applies
   bool has_scene = false;
   unsigned long long* d_counter = nullptr;
@@ -124,6 +127,7 @@ void free_scene(rt_ctx* c) {
   (void)hipFree(c->d_leaves);
   c->d_wnodes = nullptr;
   c->d_leaves = nullptr;
+  c->mixed_wide = false;
   c->n_leaves = 0;
   c->n_wnodes = 0;
   c->d_nodes = nullptr;
@@ -548,6 +552,112 @@ void rt_destroy(rt_ctx* c) {
   delete c;
 }
 
+namespace {
+
+// Mixed walks (media / frame worlds, F_MIXW): a 4-wide fp32-box tree (rt_bvh.cpp build_wide_bvh) over
+// every re-bounded subtree (an RT_BVH_ORDERED node reached from the world root through skeleton nodes
+// or frames), all in one array with one leaf table. Wide children are tagged RT_WNODE, leaves are
+// ~slot (a leaf may be a primitive, a chain, or a frame — an instance over a BVH, opened by the binary
+// walk code); each subtree's root node gets RT_WROOT and the wide root's index in `c` (device copy).
+// The walk enters the wide tree once the root's own box test passes. `host` is the unflagged rebuilt
+// tree, `dev` its validated device copy (flags added here). Sets c->d_wnodes / d_leaves and the
+// stack bound; a tree too deep for the lane stacks keeps the binary walk (no RT_WROOT marks).
+int mixed_wide_trees(rt_ctx* c, const std::vector<rt_node>& host, const std::vector<rt_node>& flat,
+                     std::vector<rt_node>& dev, int world, int ref_need) {
+  const int n = (int)dev.size();
+  if (n >= RT_WNODE) return RT_OK;  // (ids must stay clear of the RT_WNODE tag)
+  std::vector<int> roots;
+  std::vector<char> seen(2 * (size_t)n, 0);
+  std::function<void(int, bool)> find = [&](int id, bool in_ord) {
+    if (seen[2 * (size_t)id + in_ord]) return;
+    seen[2 * (size_t)id + in_ord] = 1;
+    const rt_node& x = flat[id];
+    const int ty = x.type & RT_TYPE_MASK;
+    if (ty == RT_NODE_BVH) {
+      const bool ord = (x.c & RT_BVH_ORDERED) != 0;
+      if (ord && !in_ord) roots.push_back(id);
+      find(x.a, in_ord || ord);  // (frames inside re-bounded subtrees hold subtrees of their own)
+      find(x.b, in_ord || ord);
+    } else if ((ty == RT_NODE_TRANSLATE || ty == RT_NODE_ROTATE) && !(x.type & RT_CHAIN_PRIM)) {
+      find(x.a, false);  // a frame: its child starts a new region
+    }
+  };
+  find(world, false);
+  if (roots.empty()) return RT_OK;
+  std::vector<rt_wnode> wide;
+  std::vector<int> wroot(n, -1), wneed_root(n, 0);
+  for (int r : roots) {
+    std::vector<rt_wnode> part;
+    int need = 0;
+    if (!rt::build_wide_bvh(host, r, part, &need)) return RT_OK;
+    const int base = (int)wide.size();
+    if (base + (int)part.size() > RT_WROOT_MASK) return RT_OK;
+    for (rt_wnode& w : part)
+      for (int k = 0; k < RT_WIDE; ++k)
+        if (w.child[k] >= 0) w.child[k] = (w.child[k] + base) | RT_WNODE;
+    wide.insert(wide.end(), part.begin(), part.end());
+    wroot[r] = base;
+  }
+  // the leaf table (as for the 4-wide walk): each referenced leaf once, c = its flat id
+  std::vector<rt_node> leaves;
+  std::vector<int> slot(n, -1);
+  for (rt_wnode& w : wide)
+    for (int k = 0; k < RT_WIDE; ++k) {
+      if (w.child[k] >= 0) continue;
+      const int id = ~w.child[k];
+      if (slot[id] < 0) {
+        slot[id] = (int)leaves.size();
+        leaves.push_back(flat[id]);
+        leaves.back().c = id;
+        if ((flat[id].type & RT_TYPE_MASK) == RT_NODE_MOVING_SPHERE) leaves.push_back(flat[id + 1]);
+      }
+      w.child[k] = ~slot[id];
+    }
+  // Stack bound of the mixed walk: skeleton nodes left first, re-bounded binary nodes either child
+  // first, a frame one entry, a wide node up to 3 stacked siblings (wide_node writes 3 slots) above the
+  // deepest of its children — a wide node's leaf that is a frame opens it.
+  std::vector<int> memo(n, -1);
+  std::function<int(int)> need_of;
+  std::function<int(int)> wneed = [&](int w) {
+    int deepest = 0;
+    for (int k = 0; k < RT_WIDE; ++k) {
+      const int ch = wide[w].child[k];
+      deepest = std::max(deepest, ch >= 0 ? wneed(ch & ~RT_WNODE) : need_of(leaves[~ch].c));
+    }
+    return 3 + deepest;
+  };
+  need_of = [&](int id) -> int {
+    if (memo[id] >= 0) return memo[id];
+    const rt_node& x = flat[id];
+    const int ty = x.type & RT_TYPE_MASK;
+    int r = 0;
+    if (ty == RT_NODE_BVH) {
+      if (wroot[id] >= 0) r = wneed(wroot[id]);
+      else if (x.c & RT_BVH_ORDERED) r = 1 + std::max(need_of(x.a), need_of(x.b));
+      else r = std::max(1 + need_of(x.a), need_of(x.b));
+    } else if ((ty == RT_NODE_TRANSLATE || ty == RT_NODE_ROTATE) && !(x.type & RT_CHAIN_PRIM)) {
+      r = 1 + need_of(x.a);
+    }
+    return memo[id] = r;
+  };
+  const int need = need_of(world);
+  if (need + 2 > RT_WSTACK) return RT_OK;  // (the binary walk's bound stays)
+  for (int r : roots) dev[r].c |= RT_WROOT | (wroot[r] << 2);
+  int rc;
+  if ((rc = upload(&c->d_wnodes, wide.data(), wide.size())) || (rc = upload(&c->d_leaves, leaves.data(), leaves.size())))
+    return rc;
+  HIPCHK(hipMemcpy(c->d_nodes, dev.data(), sizeof(rt_node) * dev.size(), hipMemcpyHostToDevice));
+  c->n_wnodes = (int)wide.size();
+  c->n_leaves = (int)leaves.size();
+  c->scene.wnodes = c->d_wnodes;
+  c->scene.leaves = c->d_leaves;
+  c->stack_need = std::max(need, ref_need);
+  c->mixed_wide = true;
+  return RT_OK;
+}
+
+}  // namespace
+
 int rt_upload_scene(rt_ctx* c, const rt_scene_desc* d) { return rt_upload_scene_ex(c, d, 0u); }
 
 int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
@@ -574,7 +684,7 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
     // frames) are re-bounded; RTAMD_SKELETON=0 keeps the caller's tree as is.
     dd.world_root = rt::rebuild_for_device(nodes, din->world_root);
   }
-  if ((int)nodes.size() >= RT_SUB) return invalid("rt_upload_scene: too many nodes (ids must stay below 2^29)");
+  if ((int)nodes.size() >= RT_ISBOX) return invalid("rt_upload_scene: too many nodes (ids must stay below 2^27)");
   dd.nodes = nodes.data();
   dd.n_nodes = (int)nodes.size();
   const rt_scene_desc* d = &dd;
@@ -608,6 +718,15 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
     return invalid("rt_upload_scene: image_pool is null but image_pool_bytes > 0");
   free_scene(c);
   c->rebuilt_bvh = dd.world_root != din->world_root;
+  // BVH children that are BVH nodes carry RT_ISBOX in the device copy (every walk masks it off), so
+  // that the walks' box-first scheduling knows a node's kind without loading it
+  const std::vector<rt_node> untagged = v.nodes;  // (the mixed walk's wide trees are built from it)
+  auto is_bvh = [&](int id) { return (untagged[id].type & RT_TYPE_MASK) == RT_NODE_BVH; };
+  for (rt_node& x : v.nodes)
+    if ((x.type & RT_TYPE_MASK) == RT_NODE_BVH) {
+      if (is_bvh(x.a)) x.a |= RT_ISBOX;
+      if (is_bvh(x.b)) x.b |= RT_ISBOX;
+    }
   int rc;
   if ((rc = upload(&c->d_nodes, v.nodes.data(), v.nodes.size())) ||
       (rc = upload(&c->d_mats, mats.data(), mats.size())) ||
@@ -625,8 +744,8 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
   S.perlins = c->d_perlins;
   S.images = c->d_images;
   S.pool = c->d_pool;
-  S.world = d->world_root;
-  S.world_ref = din->world_root;
+  S.world = d->world_root | (is_bvh(d->world_root) ? RT_ISBOX : 0);
+  S.world_ref = din->world_root | (is_bvh(din->world_root) ? RT_ISBOX : 0);
   S.lights = d->lights_root;
   for (int i = 0; i < 3; ++i) S.bg[i] = d->background[i];
   c->features = scene_features(d);
@@ -670,6 +789,12 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
       c->n_wnodes = (int)wide.size();
       c->wide_stack_need = std::max(need, v.stack_need[din->world_root]);
       S.wnodes = c->d_wnodes;
+    }
+  }
+  if (c->replace_ok && S.ref_walk && !env_off("RTAMD_MIXW")) {
+    if ((rc = mixed_wide_trees(c, nodes, untagged, v.nodes, d->world_root, v.stack_need[din->world_root]))) {
+      free_scene(c);
+      return rc;
     }
   }
   if (!c->d_wnodes) S.wnodes = nullptr, S.leaves = nullptr;
@@ -869,8 +994,8 @@ int rt_debug_closest_hits(rt_ctx* c, const double* rays, int n, double tmin, dou
     hipLaunchKernelGGL(closest_hits<F_ALL | F_UV | F_WIDE>, grid, dim3(RT_BLOCK), 0, c->stream, c->scene, d_rays, n,
                        tmin, tmax, seed, joint, 1, d_out);
   else
-    hipLaunchKernelGGL(closest_hits<F_ALL | F_UV>, grid, dim3(RT_BLOCK), 0, c->stream, c->scene, d_rays, n, tmin,
-                       tmax, seed, joint, (flags & RT_DEBUG_RESUMABLE) ? 1 : 0, d_out);
+    hipLaunchKernelGGL(closest_hits<F_ALL | F_UV | F_MIXW>, grid, dim3(RT_BLOCK), 0, c->stream, c->scene, d_rays, n,
+                       tmin, tmax, seed, joint, (flags & RT_DEBUG_RESUMABLE) ? 1 : 0, d_out);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipMemcpy(out, d_out, sizeof(double) * 12 * (size_t)n, hipMemcpyDeviceToHost));

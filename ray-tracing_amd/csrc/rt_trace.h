@@ -16,8 +16,13 @@ enum : unsigned {
   F_ALL = 63u | 512u,
   F_UV = 64u,     // always compute sphere (u, v) (debug queries)
   F_COUNT = 128u, // counting build: per-lane work counters (DESIGN.md "Roofline")
-  F_WIDE = 256u   // resumable walk over the 4-wide fp32-box tree (rt_wide.h) instead of the binary one
+  F_WIDE = 256u,  // resumable walk over the 4-wide fp32-box tree (rt_wide.h) instead of the binary one
+  F_MIXW = 1024u  // the mixed walk (media / frame worlds) enters 4-wide fp32-box trees built over the
+                  // re-bounded subtrees (RT_WROOT nodes) instead of walking them node by node
 };
+// fp32 ray state (Trav::o32 ...) maintained: the 4-wide walk, or the mixed walk's wide subtrees
+template <unsigned F>
+constexpr bool kRay32 = (F & (F_WIDE | F_MIXW)) != 0;
 
 // Work counters of the counting build (F_COUNT); all zero-cost otherwise.
 struct Cnt {
@@ -437,7 +442,7 @@ __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr
   int sp = 0;
   int node = root;
   for (;;) {
-    const rt_node* n = &S.nodes[node];
+    const rt_node* n = &S.nodes[node & ~RT_ISBOX];
     const int tf = n->type;
     const int type = tf & RT_TYPE_MASK;
     if (type == RT_NODE_BVH) {
@@ -550,7 +555,8 @@ struct Side {
   __device__ __forceinline__ int& best(int i) { return p[(14 + RT_MAX_FRAMES + i) * stride]; }
   __device__ __forceinline__ int best(int i) const { return p[(14 + RT_MAX_FRAMES + i) * stride]; }
 };
-constexpr int kSubChain = -1, kSubMedium = -2;  // Trav::best_sub of a chain / ConstantMedium hit
+// Trav::best_sub of a chain hit (kSubChain | the primitive's face) and of a ConstantMedium hit
+constexpr int kSubChain = 0x100, kSubMedium = -2;
 // Trav::best_node of a leaf found by the 4-wide walk: its leaf-table slot | kSlotTag, so that the
 // record is built from the (LDS-staged) leaf table rather than the flat node array in HBM
 constexpr int kSlotTag = 0x40000000;
@@ -569,7 +575,6 @@ struct Trav {
   RayX ray;
   double closest;     // closest hit so far
   double closest_up;  // the test bound: next double above `closest`, so that exact ties are seen
-  double best_tmax;   // chain hits: the bound in force when the best hit was found
   int node, sp, best_node, best_sub;
   int pend;           // F_WIDE: a postponed leaf (flat node id), -1 = none
   int level;          // F_INST: open instance frames (their ids in the lane's Side slots)
@@ -593,12 +598,44 @@ __device__ __forceinline__ float f32_upper(double x) {  // >= x (or +inf)
   return f + fabsf(f) * 0x1p-22f;
 }
 
+// The ray in fp32 for the conservative child-box test (wide_keys2), from t.ray: the 4-wide walk's
+// rays, and in the mixed walk every ray a frame opens or closes (t.tmax32 is left alone: the bound
+// is in t units, which the instance transforms keep).
+__device__ __forceinline__ void set_ray32(Trav& t, double t_min) {
+  t.o32x = (float)t.ray.o.x;
+  t.o32y = (float)t.ray.o.y;
+  t.o32z = (float)t.ray.o.z;
+  t.i32x = (float)t.ray.inv.x;
+  t.i32y = (float)t.ray.inv.y;
+  t.i32z = (float)t.ray.inv.z;
+  // K = max |o * (1/d)| over the finite axes (the origin's rounding, in t units)
+  const float kx = isinf(t.i32x) ? 0.0f : fabsf(t.o32x * t.i32x);
+  const float ky = isinf(t.i32y) ? 0.0f : fabsf(t.o32y * t.i32y);
+  const float kz = isinf(t.i32z) ? 0.0f : fabsf(t.o32z * t.i32z);
+  t.slack = fmaxf(fmaxf(kx, ky), kz) * 0x1p-20f;
+  t.tmin32 = f32_lower(t_min);
+  t.oct = (signbit(t.i32x) ? 1u : 0u) | (signbit(t.i32y) ? 2u : 0u) | (signbit(t.i32z) ? 4u : 0u);
+  // 1/d overflowing fp32 for d != 0 (|d| < 2^-126), a NaN direction, a non-finite origin, or
+  // t_min <= 0 (wide_key's scaling needs near > 0): the fp32 distances say nothing. All plane
+  // distances become 0 and the slack infinite, so every child is entered (leaves decide).
+  const bool bad = (isinf(t.i32x) & (t.ray.d.x != 0.0)) | (isinf(t.i32y) & (t.ray.d.y != 0.0)) |
+                   (isinf(t.i32z) & (t.ray.d.z != 0.0)) | isnan(t.i32x) | isnan(t.i32y) | isnan(t.i32z) |
+                   !isfinite(t.o32x) | !isfinite(t.o32y) | !isfinite(t.o32z) | isnan(t.slack) |
+                   !(t.tmin32 > 0.0f);
+  t.o32x = bad ? 0.0f : t.o32x;
+  t.o32y = bad ? 0.0f : t.o32y;
+  t.o32z = bad ? 0.0f : t.o32z;
+  t.i32x = bad ? 0.0f : t.i32x;
+  t.i32y = bad ? 0.0f : t.i32y;
+  t.i32z = bad ? 0.0f : t.i32z;
+  t.slack = bad ? INFINITY : t.slack;
+}
+
 template <unsigned F>
 __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r, int root, double t_min, double t_max) {
   t.ray = prep(r);
   t.closest = t_max;
   t.closest_up = nextafter(t_max, INFINITY);
-  t.best_tmax = t_max;
   t.node = root;
   t.sp = 0;
   t.best_node = -1;
@@ -609,36 +646,10 @@ __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r, int root, doub
   t.tie = false;
   t.ref = false;
   t.redo = false;
-  if constexpr ((F & F_WIDE) != 0) {
-    t.node = 0;  // wide root
-    t.o32x = (float)r.o.x;
-    t.o32y = (float)r.o.y;
-    t.o32z = (float)r.o.z;
-    t.i32x = (float)t.ray.inv.x;
-    t.i32y = (float)t.ray.inv.y;
-    t.i32z = (float)t.ray.inv.z;
-    // K = max |o * (1/d)| over the finite axes (the origin's rounding, in t units)
-    const float kx = isinf(t.i32x) ? 0.0f : fabsf(t.o32x * t.i32x);
-    const float ky = isinf(t.i32y) ? 0.0f : fabsf(t.o32y * t.i32y);
-    const float kz = isinf(t.i32z) ? 0.0f : fabsf(t.o32z * t.i32z);
-    t.slack = fmaxf(fmaxf(kx, ky), kz) * 0x1p-20f;
-    t.tmin32 = f32_lower(t_min);
+  if constexpr ((F & F_WIDE) != 0) t.node = 0;  // wide root
+  if constexpr (kRay32<F>) {
+    set_ray32(t, t_min);
     t.tmax32 = f32_upper(t_max);
-    t.oct = (signbit(t.i32x) ? 1u : 0u) | (signbit(t.i32y) ? 2u : 0u) | (signbit(t.i32z) ? 4u : 0u);
-    // 1/d overflowing fp32 for d != 0 (|d| < 2^-126), a NaN direction, a non-finite origin, or
-    // t_min <= 0 (wide_key's scaling needs near > 0): the fp32 distances say nothing. All plane
-    // distances become 0 and the slack infinite, so every child is entered (leaves decide).
-    const bool bad = (isinf(t.i32x) & (r.d.x != 0.0)) | (isinf(t.i32y) & (r.d.y != 0.0)) |
-                     (isinf(t.i32z) & (r.d.z != 0.0)) | isnan(t.i32x) | isnan(t.i32y) | isnan(t.i32z) |
-                     !isfinite(t.o32x) | !isfinite(t.o32y) | !isfinite(t.o32z) | isnan(t.slack) |
-                     !(t.tmin32 > 0.0f);
-    t.o32x = bad ? 0.0f : t.o32x;
-    t.o32y = bad ? 0.0f : t.o32y;
-    t.o32z = bad ? 0.0f : t.o32z;
-    t.i32x = bad ? 0.0f : t.i32x;
-    t.i32y = bad ? 0.0f : t.i32y;
-    t.i32z = bad ? 0.0f : t.i32z;
-    t.slack = bad ? INFINITY : t.slack;
   }
 }
 
@@ -652,7 +663,6 @@ __device__ __forceinline__ void trav_restart_ref(Trav& t, int root, double t_max
   t.sp = 0;
   t.closest = t_max;
   t.closest_up = t_max;
-  t.best_tmax = t_max;
   t.best_node = -1;
   t.best_sub = 0;
   t.pend = -1;
@@ -661,6 +671,7 @@ __device__ __forceinline__ void trav_restart_ref(Trav& t, int root, double t_max
   t.tie = false;
   t.ref = true;
   t.redo = redo;
+  t.tmax32 = f32_upper(t_max);  // (mixed walks: the wide subtrees' bound)
 }
 
 // Leaf of the resumable walk (a primitive, or an instance chain ending in one). Leaves are tested
@@ -676,7 +687,6 @@ __device__ __forceinline__ void trav_restart_ref(Trav& t, int root, double t_max
 template <unsigned F>
 __device__ __forceinline__ void trav_take(Trav& t, double x, int id, int sub, Side& side, bool refsem) {
   if (refsem || x < t.closest) {
-    t.best_tmax = refsem ? t.closest : t.closest_up;
     t.closest = x;
     t.closest_up = t.ref ? (kRefMixed<F> ? nextafter(x, INFINITY) : x) : nextafter(x, INFINITY);
     t.best_node = id;
@@ -685,36 +695,79 @@ __device__ __forceinline__ void trav_take(Trav& t, double x, int id, int sub, Si
       t.best_level = t.level;
       for (int k = 0; k < t.level; ++k) side.best(k) = side.frame(k);
     }
-    if constexpr ((F & F_WIDE) != 0) t.tmax32 = f32_upper(x);
+    if constexpr (kRay32<F>) t.tmax32 = f32_upper(x);
   } else if (x == t.closest && id != t.best_node) {  // (the same leaf twice is no tie)
     t.tie = true;
   }
 }
-// A leaf: a primitive, an instance chain ending in one (its t only: the record is built once, in
-// trav_finish), or a ConstantMedium (ref walks only: its one draw happens here, in the
-// reference's order and under its bound, Lib.hs:1053-1080).
+// A leaf: a primitive, an instance chain ending in one (its t and face only: the record is built once,
+// in trav_finish), or a ConstantMedium (ref walks only: its one draw happens here, in the reference's
+// order and under its bound, Lib.hs:1053-1080). The three kinds share ONE inlined primitive test
+// (prim_t): a chain or a medium's boundary chain first carries the ray down to its primitive (the
+// transforms keep the ray parameter, chain_t), a medium queries its boundary twice (t1 over
+// (-inf, inf), then t2 over (t1 + eps, inf)), so a kernel holds one copy of the primitive code in its
+// walk instead of six.
 template <unsigned F, class R>
 __device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, const rt_node* n, int id, double t_min, Cnt& cnt,
                                           R& g, Side& side, bool refsem) {
   const int type = n->type & RT_TYPE_MASK;
-  const double bound = refsem ? t.closest : t.closest_up;
-  if ((F & F_INST) && (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE)) {
-    if constexpr ((F & F_COUNT) != 0) ++cnt.other;
-    double tt;
-    const int flat = (id & kSlotTag) ? n->c : id;  // (the chain is walked in the flat node array)
-    if (chain_t<F>(S, flat, plain(t.ray), t_min, bound, tt)) trav_take<F>(t, tt, id, kSubChain, side, refsem);
-  } else if ((F & F_MEDIA) && type == RT_NODE_CONSTANT_MEDIUM) {  // (always on the skeleton: refsem)
-    if constexpr ((F & F_COUNT) != 0) ++cnt.other;
-    Hit h;
-    if (medium_hit<F>(S, n, t.ray, t_min, t.closest, g, h)) trav_take<F>(t, h.t, id, kSubMedium, side, true);
-  } else {
-    if constexpr ((F & F_COUNT) != 0) ++cnt.prim;
-    double tt;
-    int sub;
-    if (prim_t<F>(S, n, t.ray, t_min, bound, tt, sub)) {
-      if constexpr ((F & F_COUNT) != 0) ++cnt.phit;
-      trav_take<F>(t, tt, id, sub, side, refsem);
+  const bool chain = (F & F_INST) && (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE);
+  const bool medium = (F & F_MEDIA) && type == RT_NODE_CONSTANT_MEDIUM;  // (always on the skeleton: refsem)
+  if constexpr ((F & F_COUNT) != 0) {
+    if (chain || medium) ++cnt.other;
+    else ++cnt.prim;
+  }
+  const rt_node* p = n;
+  RayX rx = t.ray;
+  if constexpr ((F & (F_INST | F_MEDIA)) != 0) {
+    if (chain || medium) {
+      // (a chain is walked in the flat node array; a leaf of the 4-wide walk carries its flat id in c)
+      int cur = medium ? n->a : ((id & kSlotTag) ? n->c : id);
+      if constexpr ((F & F_INST) != 0) {
+        int ty = S.nodes[cur].type & RT_TYPE_MASK;
+        if (ty == RT_NODE_TRANSLATE || ty == RT_NODE_ROTATE) {
+          Ray r = plain(t.ray);
+          do {
+            r = enter_instance(&S.nodes[cur], r);
+            cur = S.nodes[cur].a;
+            ty = S.nodes[cur].type & RT_TYPE_MASK;
+          } while (ty == RT_NODE_TRANSLATE || ty == RT_NODE_ROTATE);
+          rx = prep(r);
+        }
+      }
+      p = &S.nodes[cur];
     }
+  }
+  double lo = medium ? -INFINITY : t_min;
+  const double hi = medium ? INFINITY : (refsem ? t.closest : t.closest_up);
+  double tt = 0.0, t1 = 0.0;
+  int sub = 0;
+  bool ok;
+#pragma nounroll
+  for (int q = 0;; ++q) {
+    ok = prim_t<F>(S, p, rx, lo, hi, tt, sub);
+    if (!(medium && ok && q == 0)) break;
+    t1 = tt;  // hit ConstantMedium's first boundary query; the second starts just past it
+    lo = t1 + kEps;
+  }
+  if (!ok) return;
+  if (!medium) {
+    if constexpr ((F & F_COUNT) != 0) cnt.phit += !chain;
+    trav_take<F>(t, tt, id, chain ? (kSubChain | sub) : sub, side, refsem);
+    return;
+  }
+  if constexpr ((F & F_MEDIA) != 0) {  // the rest of hit ConstantMedium (Lib.hs:1062-1080)
+    const Ray r = plain(t.ray);
+    const double rec1tp = gmax(t_min, t1);
+    const double rec2t = gmin(t.closest, tt);
+    if (rec1tp >= rec2t) return;
+    const double rec1t = rec1tp < 0 ? 0 : rec1tp;
+    const double ray_length = vlen(r.d);
+    const double dist_inside = (rec2t - rec1t) * ray_length;
+    const double rnd = g.draw();
+    const double hit_dist = n->f[0] * log(rnd);
+    if (hit_dist > dist_inside) return;
+    trav_take<F>(t, rec1t + (hit_dist / ray_length), id, kSubMedium, side, true);
   }
 }
 
@@ -756,10 +809,10 @@ __device__ __forceinline__ void cswap(float& ka, int& ca, float& kb, int& cb) {
   ca = c;
 }
 
-// One wide node: test the four child boxes, enter the nearest accepted child, stack the others
-// (farthest deepest).
-__device__ __forceinline__ bool wide_node(const Scene& S, Trav& t, int* stk, int stride) {
-  const float* base = reinterpret_cast<const float*>(&S.wnodes[t.node]);
+// One wide node (index `w`): test the four child boxes, enter the nearest accepted child, stack the
+// others (farthest deepest).
+__device__ __forceinline__ bool wide_node(const Scene& S, Trav& t, int* stk, int stride, int w) {
+  const float* base = reinterpret_cast<const float*>(&S.wnodes[w]);
   const int ox = (t.oct & 1u) ? 12 : 0, oy = (t.oct & 2u) ? 16 : 4, oz = (t.oct & 4u) ? 20 : 8;
   const float4 nx = *reinterpret_cast<const float4*>(base + ox);
   const float4 ny = *reinterpret_cast<const float4*>(base + oy);
@@ -792,6 +845,33 @@ __device__ __forceinline__ bool wide_node(const Scene& S, Trav& t, int* stk, int
   return n_hit != 0;
 }
 
+// Pop the next node of a binary (or mixed) walk; false once the walk is over. Frames that close
+// rebuild the parent's ray from the world ray, once for a run of them. (Mixed walks: leaf slots are
+// negative, so only a non-negative entry can be a frame marker.)
+template <unsigned F>
+__device__ __forceinline__ bool trav_pop_mixed(const Scene& S, Trav& t, const int* stk, int stride, Side& side,
+                                               double t_min = kEps) {
+  bool reb = false;
+  Ray pr;
+  for (;;) {
+    const bool end = t.sp == 0;
+    const int e = end ? 0 : stk[(--t.sp) * stride];
+    const bool frame = (F & F_FRAMES) && ((F & F_MIXW) ? (e >= 0 && (e & RT_FRAME)) : (e & RT_FRAME));
+    if (end || !frame) {
+      if ((F & F_FRAMES) && reb) {  // (also at the end: a tie redo walks on from it)
+        t.ray = prep(pr);
+        if constexpr ((F & F_MIXW) != 0) set_ray32(t, t_min);
+      }
+      t.node = e;
+      return !end;
+    }
+    --t.level;  // a frame closes
+    reb = true;
+    pr = side.get_ray();
+    for (int k = 0; k < t.level; ++k) pr = enter_instance(&S.nodes[side.frame(k)], pr);
+  }
+}
+
 // Visit one node; false once the walk is over. The binary walk also opens instance frames
 // (Translate/Rotate over a BVH, Lib.hs:1029-1052): a tagged stack entry, the frame's id in the
 // lane's Side slots, and the child's ray in Trav::ray; when the entry is popped the parent's ray is
@@ -804,7 +884,7 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
   if (wide) {
     if (t.node >= 0) {
       if constexpr ((F & F_COUNT) != 0) ++cnt.wide;
-      if (wide_node(S, t, stk, stride)) return true;
+      if (wide_node(S, t, stk, stride, t.node)) return true;
     } else {
       const rt_node* n = &S.leaves[~t.node];
       trav_leaf<F>(S, t, n, ~t.node | kSlotTag, t_min, cnt, g, side, false);
@@ -813,18 +893,36 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
     t.node = stk[(--t.sp) * stride];
     return true;
   }
+  // Mixed walks with wide subtrees (F_MIXW): a node is a flat id (| RT_SUB), a wide node
+  // (RT_WNODE | index) or a leaf-table slot handed out by a wide node (~slot, negative); all of them
+  // lie in re-bounded subtrees except flat ids without RT_SUB.
+  bool leaf_slot = false;
+  if constexpr ((F & F_MIXW) != 0) {
+    if (t.node >= 0 && (t.node & RT_WNODE)) {
+      if constexpr ((F & F_COUNT) != 0) ++cnt.wide;
+      if (wide_node(S, t, stk, stride, t.node & ~RT_WNODE)) return true;
+      return trav_pop_mixed<F>(S, t, stk, stride, side);
+    }
+    leaf_slot = t.node < 0;
+  }
   // (mixed walks: the RT_SUB tag of the node id says whether it lies below an RT_BVH_ORDERED node)
-  const int id = kRefMixed<F> ? (t.node & ~RT_SUB) : t.node;
-  const int tag = kRefMixed<F> ? (t.node & RT_SUB) : 0;
+  const int id = leaf_slot ? (~t.node | kSlotTag) : (t.node & ~(RT_SUB | RT_ISBOX));
+  const int tag = leaf_slot ? RT_SUB : (kRefMixed<F> ? (t.node & RT_SUB) : 0);
   const bool refsem = t.ref && !tag;
-  const rt_node* n = &S.nodes[id];
+  const rt_node* n = leaf_slot ? &S.leaves[~t.node] : &S.nodes[id];
   const int tf = n->type;
   const int type = tf & RT_TYPE_MASK;
-  if (type == RT_NODE_BVH) {
+  if (type == RT_NODE_BVH) {  // (never a leaf slot)
     if constexpr ((F & F_COUNT) != 0) ++cnt.box;
     if (box_hit(n->f, t.ray, t_min, refsem ? t.closest : t.closest_up, joint)) {
       const int c = n->c;
       const bool ord = (c & RT_BVH_ORDERED) && !t.redo;
+      if constexpr ((F & F_MIXW) != 0) {
+        if (ord && (c & RT_WROOT)) {  // a re-bounded subtree with a 4-wide tree: walk that instead
+          t.node = RT_WNODE | ((c >> 2) & RT_WROOT_MASK);
+          return true;
+        }
+      }
       const bool flip = ord && comp(t.ray.d, c & 3) < 0;
       const int ctag = (kRefMixed<F> && ord) ? RT_SUB : tag;
       stk[(t.sp++) * stride] = (flip ? n->a : n->b) | ctag;
@@ -832,28 +930,28 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
       return true;
     }
   } else if ((F & F_FRAMES) && (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE) && !(tf & RT_CHAIN_PRIM)) {
-    if constexpr ((F & F_COUNT) != 0) ++cnt.other;
     if (t.level == 0) side.put_ray(plain(t.ray));
-    side.frame(t.level++) = id;
-    stk[(t.sp++) * stride] = RT_FRAME | id;
-    t.ray = prep(enter_instance(n, plain(t.ray)));
-    t.node = n->a | tag;
+    // consecutive instances over a BVH (e.g. translate (rotate bvh)) open their frames in one step,
+    // with one prep() for the innermost ray (the outer frames' rays are not tested against anything)
+    Ray cr = plain(t.ray);
+    int cur = leaf_slot ? n->c : id, ct = tf;
+    do {
+      if constexpr ((F & F_COUNT) != 0) ++cnt.other;
+      side.frame(t.level++) = cur;
+      stk[(t.sp++) * stride] = RT_FRAME | cur;
+      cr = enter_instance(&S.nodes[cur], cr);
+      cur = S.nodes[cur].a;
+      ct = S.nodes[cur].type;
+    } while (((ct & RT_TYPE_MASK) == RT_NODE_TRANSLATE || (ct & RT_TYPE_MASK) == RT_NODE_ROTATE) &&
+             !(ct & RT_CHAIN_PRIM));
+    t.ray = prep(cr);
+    if constexpr ((F & F_MIXW) != 0) set_ray32(t, t_min);
+    t.node = cur | tag;
     return true;
   } else {
     trav_leaf<F>(S, t, n, id, t_min, cnt, g, side, refsem);
   }
-  for (;;) {
-    if (t.sp == 0) return false;
-    const int e = stk[(--t.sp) * stride];
-    if (!(F & F_FRAMES) || !(e & RT_FRAME)) {
-      t.node = e;
-      return true;
-    }
-    --t.level;  // a frame closes
-    Ray pr = side.get_ray();
-    for (int k = 0; k < t.level; ++k) pr = enter_instance(&S.nodes[side.frame(k)], pr);
-    t.ray = prep(pr);
-  }
+  return trav_pop_mixed<F>(S, t, stk, stride, side, t_min);
 }
 
 // ---- the 4-wide walk with postponed leaves (Aila & Laine's while-while, one postponed slot)
@@ -877,7 +975,7 @@ __device__ __forceinline__ void trav_postpone(Trav& t, const int* stk, int strid
 template <unsigned F>
 __device__ __forceinline__ void wide_inner(const Scene& S, Trav& t, int* stk, int stride, Cnt& cnt) {
   if constexpr ((F & F_COUNT) != 0) ++cnt.wide;
-  if (!wide_node(S, t, stk, stride)) t.node = trav_pop(t, stk, stride);
+  if (!wide_node(S, t, stk, stride, t.node)) t.node = trav_pop(t, stk, stride);
   trav_postpone(t, stk, stride);
 }
 template <unsigned F, class R>
@@ -907,19 +1005,30 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
       // (box-first steps only in the full variant's kernels, whose steps mix node kinds; elsewhere the
       // node-kind read and ballots would be overhead: C3 357 ms either way)
       constexpr bool kBoxFirst = kRefMixed<F> || (F & F_COUNT) != 0;
-      const int ty = (kBoxFirst && walking) ? (S.nodes[kRefMixed<F> ? (t.node & ~RT_SUB) : t.node].type & RT_TYPE_MASK)
-                                            : -1;
-      const bool at_box = ty == RT_NODE_BVH;
-      const bool box_only = kBoxFirst && leaf_stop < n_walk && __popcll(__ballot(at_box)) > leaf_stop;
+      // (BVH nodes and wide nodes carry their kind in the id: RT_ISBOX, RT_WNODE; a wide node's leaf is
+      // negative; the counting build also reads the other kinds)
+      const bool at_box = kBoxFirst && walking && t.node >= 0 && (t.node & (RT_ISBOX | RT_WNODE));
+      int ty = -1;
+      if constexpr ((F & F_COUNT) != 0) {
+        if (walking) {
+          if ((F & F_MIXW) && t.node < 0) ty = S.leaves[~t.node].type & RT_TYPE_MASK;
+          else if (at_box) ty = RT_NODE_BVH;
+          else ty = S.nodes[t.node & ~(RT_SUB | RT_ISBOX)].type & RT_TYPE_MASK;
+        }
+      }
+      bool go = walking;
+      if constexpr (kBoxFirst) {
+        const int n_box = __popcll(__ballot(at_box));
+        if (leaf_stop < n_walk && n_box > leaf_stop) go = walking && at_box;
+      }
       if constexpr ((F & F_COUNT) != 0) {  // counting build: wave steps, and the node kinds each one runs
         ++cnt.islot;                        // (every lane counts a step: / 64 per wave)
         const bool inst = ty == RT_NODE_TRANSLATE || ty == RT_NODE_ROTATE;
-        const bool go = walking && (at_box || !box_only);
         cnt.lslot += (__ballot(go && at_box) != 0) + (__ballot(go && inst) != 0) +
                      (__ballot(go && ty == RT_NODE_CONSTANT_MEDIUM) != 0) +
                      (__ballot(go && !at_box && !inst && ty != RT_NODE_CONSTANT_MEDIUM) != 0);
       }
-      if (walking && (!box_only || at_box)) walking = trav_step<F>(S, t, t_min, stk, stride, joint, cnt, g, side);
+      if (go) walking = trav_step<F>(S, t, t_min, stk, stride, joint, cnt, g, side);
     }
   } else {
     for (;;) {
@@ -947,51 +1056,70 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
   }
 }
 
-// The closest hit's record, built once from the same ray with the same operations (a chain
-// hit is re-run under the bound that was in force when it was found; a medium's record is its
-// t, the point on the ray, normal (1,0,0), u = v = 0, front face, Lib.hs:1074-1080). A hit inside
-// instance frames is recorded in the innermost frame's ray, then each frame's rewrite is applied
-// from the innermost outwards with the ray its child saw (as `traverse` does when frames close).
-// `r` is the world ray. Callers check `tie` first and re-walk with trav_restart_ref.
-template <unsigned F>
-__device__ __forceinline__ bool leaf_record(const Scene& S, const Trav& t, const Ray& r, double t_min, Hit& h) {
-  // (a leaf of the 4-wide walk: its record from the leaf table)
-  const bool slot = (F & F_WIDE) && (t.best_node & kSlotTag);
-  const rt_node* n = slot ? &S.leaves[t.best_node & ~kSlotTag] : &S.nodes[t.best_node];
-  if constexpr ((F & F_INST) != 0)
-    if (t.best_sub == kSubChain) return chain_hit<F>(S, slot ? n->c : t.best_node, r, t_min, t.best_tmax, h);
-  if constexpr ((F & F_MEDIA) != 0)
-    if (t.best_sub == kSubMedium) {
-      h.t = t.closest;
-      h.p = at(r, t.closest);
-      h.n = v3(1, 0, 0);
-      h.u = 0;
-      h.v = 0;
-      h.ff = 1;
-      h.mat = S.nodes[t.best_node].b;
-      return true;
-    }
-  prim_record<F>(S, n, t.best_sub, r, t.closest, h);
-  return true;
-}
+// The closest hit's record, built once from the same ray with the same operations (a chain hit's
+// primitive in the chain's innermost frame, with the t and face the walk found; a medium's record is
+// its t, the point on the ray, normal (1,0,0), u = v = 0, front face, Lib.hs:1074-1080). A hit inside
+// instance frames is recorded in the innermost frame's ray, then each frame's rewrite is applied from
+// the innermost outwards with the ray its child saw (as `traverse` does when frames close); a chain's
+// instances likewise (chain_hit). `r` is the world ray. Callers check `tie` first and re-walk with
+// trav_restart_ref. One inlined copy of the record code (prim_record) per kernel.
 template <unsigned F>
 __device__ __forceinline__ bool trav_finish(const Scene& S, const Trav& t, const Ray& r, double t_min, Hit& h,
                                             const Side& side) {
   if (t.best_node < 0) return false;
-  if constexpr ((F & F_FRAMES) != 0) {
-    if (t.best_level > 0) {
-      Ray fr = r;
-      for (int k = 0; k < t.best_level; ++k) fr = enter_instance(&S.nodes[side.best(k)], fr);
-      leaf_record<F>(S, t, fr, t_min, h);
-      for (int lv = t.best_level - 1; lv >= 0; --lv) {
-        Ray rc = r;  // the ray frame lv's child saw
-        for (int k = 0; k <= lv; ++k) rc = enter_instance(&S.nodes[side.best(k)], rc);
-        exit_instance(&S.nodes[side.best(lv)], rc, h);
+  // (a leaf of the 4-wide walk: its record from the leaf table)
+  const bool slot = (F & (F_WIDE | F_MIXW)) && (t.best_node & kSlotTag);
+  const rt_node* n = slot ? &S.leaves[t.best_node & ~kSlotTag] : &S.nodes[t.best_node];
+  int levels = 0;  // frames around the hit, then the chain's instances
+  if constexpr ((F & F_FRAMES) != 0) levels = t.best_level;
+  Ray fr = r;  // the ray in the hit primitive's (or medium's) frame
+  int sub = t.best_sub;
+  const rt_node* leaf = n;
+  int chain_id = -1, chain_len = 0;
+  if constexpr ((F & F_FRAMES) != 0)
+    for (int k = 0; k < levels; ++k) fr = enter_instance(&S.nodes[side.best(k)], fr);
+  bool med = false;
+  if constexpr ((F & F_MEDIA) != 0) med = sub == kSubMedium;
+  if (med) {
+    h.t = t.closest;
+    h.p = at(fr, t.closest);
+    h.n = v3(1, 0, 0);
+    h.u = 0;
+    h.v = 0;
+    h.ff = 1;
+    h.mat = S.nodes[t.best_node].b;
+  }
+  if constexpr ((F & F_INST) != 0) {
+    if (!med && (sub & kSubChain)) {
+      sub &= ~kSubChain;
+      chain_id = slot ? n->c : t.best_node;
+      int cur = chain_id;
+      while ((S.nodes[cur].type & RT_TYPE_MASK) == RT_NODE_TRANSLATE || (S.nodes[cur].type & RT_TYPE_MASK) == RT_NODE_ROTATE) {
+        fr = enter_instance(&S.nodes[cur], fr);
+        cur = S.nodes[cur].a;
+        ++chain_len;
       }
-      return true;
+      leaf = &S.nodes[cur];
     }
   }
-  return leaf_record<F>(S, t, r, t_min, h);
+  if (!med) prim_record<F>(S, leaf, sub, fr, t.closest, h);
+  // rewrites from the innermost instance outwards: the chain's (innermost), then the frames'
+  for (int lv = levels + chain_len - 1; lv >= 0; --lv) {
+    Ray rl = r;  // the ray instance lv's child saw
+    const rt_node* inst = nullptr;
+    int cur = chain_id;
+    for (int k = 0; k <= lv; ++k) {
+      if ((F & F_FRAMES) && k < levels) {
+        inst = &S.nodes[side.best(k)];
+      } else {
+        inst = &S.nodes[cur];
+        cur = inst->a;
+      }
+      rl = enter_instance(inst, rl);
+    }
+    exit_instance(inst, rl, h);
+  }
+  return true;
 }
 
 // ------------------------------------------------------------------ lights (Lib.hs:662-724)
@@ -1001,6 +1129,7 @@ __device__ __forceinline__ bool trav_finish(const Scene& S, const Trav& t, const
 // the same value: pdf(BVH) = box ? wl*(pdf(l)+0) + wr*(pdf(r)+0) : 0. Depth <= RT_LIGHT_DEPTH.
 template <unsigned F, int D>
 __device__ __forceinline__ double htbl_pdf_value(const Scene& S, int id, V3 origin, V3 v, const RayX& r) {
+  id &= ~RT_ISBOX;
   const rt_node* n = &S.nodes[id];
   const int type = n->type & RT_TYPE_MASK;
   Hit hh;
@@ -1023,9 +1152,9 @@ __device__ __forceinline__ double htbl_pdf_value(const Scene& S, int id, V3 orig
     if (type == RT_NODE_BVH) {
       if (!box_hit(n->f, r, kEps, INFINITY, false)) return 0.0;
       const double left_pdf = htbl_pdf_value<F, D - 1>(S, n->a, origin, v, r) + 0;
-      const double left_w = (double)S.nodes[n->a].c / (double)n->c;
+      const double left_w = (double)S.nodes[n->a & ~RT_ISBOX].c / (double)n->c;
       const double right_pdf = htbl_pdf_value<F, D - 1>(S, n->b, origin, v, r) + 0;
-      const double right_w = (double)S.nodes[n->b].c / (double)n->c;
+      const double right_w = (double)S.nodes[n->b & ~RT_ISBOX].c / (double)n->c;
       return left_w * left_pdf + right_w * right_pdf;
     }
   }
@@ -1035,10 +1164,11 @@ __device__ __forceinline__ double htbl_pdf_value(const Scene& S, int id, V3 orig
 // htblRandom (Lib.hs:707-724)
 template <class R>
 __device__ inline V3 htbl_random(const Scene& S, int id, V3 o, R& g) {
+  if (id >= 0) id &= ~RT_ISBOX;
   while (id >= 0 && (S.nodes[id].type & RT_TYPE_MASK) == RT_NODE_BVH) {
     const rt_node* n = &S.nodes[id];
     const double rd = g.draw();
-    id = rd < (double)S.nodes[n->a].c / (double)n->c ? n->a : n->b;
+    id = (rd < (double)S.nodes[n->a & ~RT_ISBOX].c / (double)n->c ? n->a : n->b) & ~RT_ISBOX;
   }
   if (id < 0) return v3(1, 0, 0);
   const rt_node* n = &S.nodes[id];
@@ -1094,6 +1224,26 @@ __device__ __forceinline__ double schlick(double cosine, double ref_idx) {
   return r1 + (1.0 - r1) * pow5(1 - cosine);
 }
 
+// textureValue of a shaded hit's material, evaluated once per shaded hit so that a kernel holds one
+// inlined copy of the texture code (Perlin turbulence is ~1.7 k instructions): every material but
+// Dielectric reads its texture (Lib.hs:822-885), DiffuseLight only on back faces (`emitted`: front
+// faces are black). Texture values draw no random numbers, so where they are evaluated changes
+// nothing else.
+// Kernels without non-constant textures (no F_TEX) read the constant where it is used instead (one
+// load; hoisting it would only keep three more doubles live across the shading code).
+template <unsigned F>
+__device__ __forceinline__ V3 hit_texture(const Scene& S, const DMat& m, const Hit& h) {
+  if constexpr ((F & F_TEX) == 0) return v3(0, 0, 0);
+  const bool need = m.type != RT_MAT_DIELECTRIC && !(m.type == RT_MAT_DIFFUSE_LIGHT && h.ff);
+  return need ? texture_value<F>(S, m.tex, h.u, h.v, h.p) : v3(0, 0, 0);
+}
+// The material's texture value at the hit: hit_texture's (F_TEX kernels) or the constant, read here.
+template <unsigned F>
+__device__ __forceinline__ V3 mat_texture(const Scene& S, const DMat& m, const Hit& h, V3 tx) {
+  if constexpr ((F & F_TEX) != 0) return tx;
+  return texture_value<F>(S, m.tex, h.u, h.v, h.p);
+}
+
 struct Scatter {
   Ray ray;
   V3 att;
@@ -1108,9 +1258,11 @@ struct Scatter {
 // Lib.hs:1187-1197) both draw two numbers and take the cosine and sine of 2*pi*(first draw) —
 // `2.0 * pi * r1` and `aa * 2.0 * pi` round identically, doubling being exact — and one square
 // root; Metal and Dielectric both start from `unit(r.d)`. Each lane's draws keep the reference's
-// order (Lambertian: coin, then its branch's draws).
+// order (Lambertian: coin, then its branch's draws). `tx` is the material's textureValue at the hit
+// (hit_texture), evaluated once by the caller.
 template <unsigned F, class R>
-__device__ __forceinline__ void scatter(const Scene& S, const DMat& m, const Ray& r, const Hit& h, R& g, Scatter& s) {
+__device__ __forceinline__ void scatter(const Scene& S, const DMat& m, const Ray& r, const Hit& h, R& g, Scatter& s,
+                                        V3 tx) {
   s.ray.o = h.p;
   s.ray.tm = r.tm;
   g.reserve(3);  // Lambertian draws 1 or 3 (more when sampling a lights BVH), Metal 2, Dielectric 1
@@ -1118,7 +1270,7 @@ __device__ __forceinline__ void scatter(const Scene& S, const DMat& m, const Ray
   const bool diel = m.type == RT_MAT_DIELECTRIC;
   if (!(lamb || metal || diel)) {  // RT_MAT_ISOTROPIC, Lib.hs:861-865
     s.ray.d = random_in_unit_sphere(g);
-    s.att = texture_value<F>(S, m.tex, h.u, h.v, h.p);
+    s.att = mat_texture<F>(S, m, h, tx);
     s.pdf = 1.0;
     s.specular = 0;
     return;
@@ -1144,7 +1296,7 @@ __device__ __forceinline__ void scatter(const Scene& S, const DMat& m, const Ray
   V3 ud = v3(0, 0, 0);
   if (metal || diel) ud = unit(r.d);
   if (lamb) {
-    s.att = texture_value<F>(S, m.tex, h.u, h.v, h.p);
+    s.att = mat_texture<F>(S, m, h, tx);
     V3 pdf_d = v;
     if constexpr ((F & F_LIGHTS) != 0)
       if (light) pdf_d = htbl_random(S, S.lights, h.p, g);
@@ -1160,7 +1312,7 @@ __device__ __forceinline__ void scatter(const Scene& S, const DMat& m, const Ray
   } else if (metal) {  // Lib.hs:837-841
     const V3 reflected = reflect(ud, h.n);
     s.ray.d = reflected + scale(m.param, v);
-    s.att = texture_value<F>(S, m.tex, h.u, h.v, h.p);
+    s.att = mat_texture<F>(S, m, h, tx);
     s.pdf = 0.0;
     s.specular = 1;
   } else {  // Dielectric, Lib.hs:842-859
