@@ -687,6 +687,9 @@ __device__ __forceinline__ void trav_restart_ref(Trav& t, int root, double t_max
 template <unsigned F>
 __device__ __forceinline__ void trav_take(Trav& t, double x, int id, int sub, Side& side, bool refsem) {
   if (refsem || x < t.closest) {
+    // (a tie at the old closest no longer matters: only leaves hit at the final closest t compete, and
+    // the bound the walk carried on with was the same whichever tied leaf won)
+    t.tie = false;
     t.closest = x;
     t.closest_up = t.ref ? (kRefMixed<F> ? nextafter(x, INFINITY) : x) : nextafter(x, INFINITY);
     t.best_node = id;
