@@ -401,7 +401,8 @@ typedef struct rt_launch_info {
     int32_t dyn_lds_bytes;
     int64_t work_items;
     int32_t chunk;
-    int32_t _pad;
+    int32_t wide_nodes;  /* 4-wide nodes the launched walk uses: the 4-wide world tree (loop 2), or the
+                            mixed walk's trees over re-bounded subtrees (loop 1, media / frame worlds) */
 } rt_launch_info;
 int rt_last_launch(rt_ctx* ctx, rt_launch_info* out);
 

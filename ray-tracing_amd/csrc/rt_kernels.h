@@ -421,6 +421,9 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
       if constexpr ((F & F_COUNT) != 0) ++cnt.ties;
       if constexpr (kRefMixed<F>) g.rewind(walk_mark);  // (the walk's media draws repeat)
       trav_restart_ref(t, S.world_ref, INFINITY, true);
+      // (the redo's binary box tests need 1/d: recomputed here, the same values, so that the 4-wide
+      // walk need not carry Trav::ray.inv)
+      if constexpr ((F & F_WIDE) != 0) t.ray = prep(plain(t.ray));
       walking = true;
     }
     // the next walk's ray: a scattered ray (next segment) or a camera ray (next sample), parked in

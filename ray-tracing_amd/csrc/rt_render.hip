@@ -470,7 +470,8 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
       int n_items = items;
       void* args[] = {&A, &n_items, (void*)&entries, &n_leaves};
       c->last_launch = rt_launch_info{var | (loop == 2 ? F_WIDE : 0u), loop, 1, n_leaves > 0, waves, c->cu_count,
-                                      block, (int)bytes, A.work_total, A.chunk, 0};
+                                      block, (int)bytes, A.work_total, A.chunk,
+                                      (loop == 2 || (loop == 1 && c->mixed_wide)) ? c->n_wnodes : 0};
       HIPCHK(hipEventRecord(c->ev0, st));
       HIPCHK(hipLaunchKernel(fn, dim3(c->cu_count), dim3(block), args, bytes, st));
       HIPCHK(hipEventRecord(c->ev1, st));
@@ -488,7 +489,8 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   const long long resident = (long long)c->cu_count * std::max(1, bpc);
   const int grid = (int)std::max(1ll, std::min(want, resident));
   c->last_launch = rt_launch_info{var | (loop == 2 ? F_WIDE : 0u) | (count ? F_COUNT : 0u), loop, 0, 0,
-                                  count ? 1 : waves, grid, RT_BLOCK, (int)dyn, A.work_total, A.chunk, 0};
+                                  count ? 1 : waves, grid, RT_BLOCK, (int)dyn, A.work_total, A.chunk,
+                                  (loop == 2 || (loop == 1 && c->mixed_wide)) ? c->n_wnodes : 0};
   HIPCHK(hipEventRecord(c->ev0, st));
   void* args[] = {&A, &entries};
   HIPCHK(hipLaunchKernel(fn, dim3(grid), dim3(RT_BLOCK), args, dyn, st));

@@ -215,6 +215,17 @@ __device__ __forceinline__ bool sphere_t(V3 sc, double sr, const RayX& r, double
   else return false;
   return true;
 }
+// A sphere hit's (u, v) from its outward normal (Lib.hs:1100-1104). Not inlined: OCML's fp64 atan and
+// asin bring polynomial coefficients that, inlined into a render loop, the compiler materialises once
+// for the whole loop and spills (the full variant: 560 -> ~290 B/lane of scratch); as a call they are
+// materialised per call, and only image-textured hits make it.
+__device__ __noinline__ void sphere_uv(V3 outward, double& u, double& v) {
+  const double phi = ghc_atan2(outward.z, outward.x);
+  const double theta = asin(outward.y);
+  u = 1.0 - ((phi + kPi) / (2 * kPi));
+  v = (theta + (kPi / 2)) / kPi;
+}
+
 // the rest of hit Sphere (Lib.hs:1096-1105)
 template <unsigned F>
 __device__ __forceinline__ void sphere_record(const Scene& S, V3 sc, double sr, int sm, const Ray& r, double t,
@@ -225,10 +236,7 @@ __device__ __forceinline__ void sphere_record(const Scene& S, V3 sc, double sr, 
   face_normal(r, outward, h.ff, h.n);
   h.mat = sm;
   if ((F & F_UV) || ((F & F_TEX) && S.mats[sm].needs_uv)) {  // u, v only feed image textures
-    const double phi = ghc_atan2(outward.z, outward.x);
-    const double theta = asin(outward.y);
-    h.u = 1.0 - ((phi + kPi) / (2 * kPi));
-    h.v = (theta + (kPi / 2)) / kPi;
+    sphere_uv(outward, h.u, h.v);
   } else {
     h.u = 0.0;
     h.v = 0.0;
@@ -574,7 +582,6 @@ constexpr bool kRefMixed = (F & (F_MEDIA | F_FRAMES)) != 0;
 struct Trav {
   RayX ray;
   double closest;     // closest hit so far
-  double closest_up;  // the test bound: next double above `closest`, so that exact ties are seen
   int node, sp, best_node, best_sub;
   int pend;           // F_WIDE: a postponed leaf (flat node id), -1 = none
   int level;          // F_INST: open instance frames (their ids in the lane's Side slots)
@@ -586,8 +593,14 @@ struct Trav {
   // F_WIDE: the ray in fp32 for the conservative child-box test (wide_keys2)
   float o32x, o32y, o32z, i32x, i32y, i32z;
   float slack, tmin32, tmax32;  // slack = +inf: the fp32 distances say nothing, accept every child
-  unsigned oct;   // bit a: the ray runs towards -axis a (its near plane is the box's hi)
 };
+
+// The leaf-test bound of a walk that flags exact ties: nextafter(closest, +inf) (+inf stays +inf), so
+// that a second leaf hit at exactly `closest` is seen. A reference walk
+// of a media-free world (a tie redo) bounds by `closest` itself. Derived, not stored (two registers
+// fewer across the walk).
+template <unsigned F>
+__device__ __forceinline__ double closest_up(const Trav& t);
 
 __device__ __forceinline__ float f32_lower(double x) {  // <= x (or -inf)
   const float f = (float)x;
@@ -614,7 +627,6 @@ __device__ __forceinline__ void set_ray32(Trav& t, double t_min) {
   const float kz = isinf(t.i32z) ? 0.0f : fabsf(t.o32z * t.i32z);
   t.slack = fmaxf(fmaxf(kx, ky), kz) * 0x1p-20f;
   t.tmin32 = f32_lower(t_min);
-  t.oct = (signbit(t.i32x) ? 1u : 0u) | (signbit(t.i32y) ? 2u : 0u) | (signbit(t.i32z) ? 4u : 0u);
   // 1/d overflowing fp32 for d != 0 (|d| < 2^-126), a NaN direction, a non-finite origin, or
   // t_min <= 0 (wide_key's scaling needs near > 0): the fp32 distances say nothing. All plane
   // distances become 0 and the slack infinite, so every child is entered (leaves decide).
@@ -635,7 +647,6 @@ template <unsigned F>
 __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r, int root, double t_min, double t_max) {
   t.ray = prep(r);
   t.closest = t_max;
-  t.closest_up = nextafter(t_max, INFINITY);
   t.node = root;
   t.sp = 0;
   t.best_node = -1;
@@ -653,6 +664,14 @@ __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r, int root, doub
   }
 }
 
+template <unsigned F>
+__device__ __forceinline__ double closest_up(const Trav& t) {
+  const double c = t.closest;
+  const long long b = __double_as_longlong(c);
+  const double up = isinf(c) ? c : (c > 0 ? __longlong_as_double(b + 1) : (c < 0 ? __longlong_as_double(b - 1) : 0x1p-1074));
+  return (!kRefMixed<F> && t.ref) ? t.closest : up;
+}
+
 // Redo the walk as the reference does it: the caller's tree, left child first, every accepted hit
 // replacing the best under bound = closest. `redo` (a walk redone for an exact tie) applies those
 // semantics to every node: a caller's tree may itself hold RT_BVH_ORDERED nodes (rt_rebuild_bvh
@@ -662,7 +681,6 @@ __device__ __forceinline__ void trav_restart_ref(Trav& t, int root, double t_max
   t.node = root;
   t.sp = 0;
   t.closest = t_max;
-  t.closest_up = t_max;
   t.best_node = -1;
   t.best_sub = 0;
   t.pend = -1;
@@ -691,7 +709,6 @@ __device__ __forceinline__ void trav_take(Trav& t, double x, int id, int sub, Si
     // the bound the walk carried on with was the same whichever tied leaf won)
     t.tie = false;
     t.closest = x;
-    t.closest_up = t.ref ? (kRefMixed<F> ? nextafter(x, INFINITY) : x) : nextafter(x, INFINITY);
     t.best_node = id;
     t.best_sub = sub;
     if constexpr ((F & F_FRAMES) != 0) {
@@ -742,7 +759,7 @@ __device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, const rt_node
     }
   }
   double lo = medium ? -INFINITY : t_min;
-  const double hi = medium ? INFINITY : (refsem ? t.closest : t.closest_up);
+  const double hi = medium ? INFINITY : (refsem ? t.closest : closest_up<F>(t));
   double tt = 0.0, t1 = 0.0;
   int sub = 0;
   bool ok;
@@ -816,7 +833,8 @@ __device__ __forceinline__ void cswap(float& ka, int& ca, float& kb, int& cb) {
 // others (farthest deepest).
 __device__ __forceinline__ bool wide_node(const Scene& S, Trav& t, int* stk, int stride, int w) {
   const float* base = reinterpret_cast<const float*>(&S.wnodes[w]);
-  const int ox = (t.oct & 1u) ? 12 : 0, oy = (t.oct & 2u) ? 16 : 4, oz = (t.oct & 4u) ? 20 : 8;
+  // (a ray running towards -axis a has the box's hi as its near plane on that axis)
+  const int ox = signbit(t.i32x) ? 12 : 0, oy = signbit(t.i32y) ? 16 : 4, oz = signbit(t.i32z) ? 20 : 8;
   const float4 nx = *reinterpret_cast<const float4*>(base + ox);
   const float4 ny = *reinterpret_cast<const float4*>(base + oy);
   const float4 nz = *reinterpret_cast<const float4*>(base + oz);
@@ -917,7 +935,7 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
   const int type = tf & RT_TYPE_MASK;
   if (type == RT_NODE_BVH) {  // (never a leaf slot)
     if constexpr ((F & F_COUNT) != 0) ++cnt.box;
-    if (box_hit(n->f, t.ray, t_min, refsem ? t.closest : t.closest_up, joint)) {
+    if (box_hit(n->f, t.ray, t_min, refsem ? t.closest : closest_up<F>(t), joint)) {
       const int c = n->c;
       const bool ord = (c & RT_BVH_ORDERED) && !t.redo;
       if constexpr ((F & F_MIXW) != 0) {

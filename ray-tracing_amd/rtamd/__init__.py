@@ -96,7 +96,7 @@ class rt_camera(C.Structure):
 class rt_launch_info(C.Structure):
     _fields_ = [("variant", C.c_uint32), ("loop", C.c_int32), ("lds_staged", C.c_int32), ("leaf_lds", C.c_int32),
                 ("waves", C.c_int32), ("grid", C.c_int32), ("block", C.c_int32), ("dyn_lds_bytes", C.c_int32),
-                ("work_items", C.c_int64), ("chunk", C.c_int32), ("_pad", C.c_int32)]
+                ("work_items", C.c_int64), ("chunk", C.c_int32), ("wide_nodes", C.c_int32)]
 
 
 class rt_render_params(C.Structure):
@@ -540,7 +540,7 @@ class Context:
         staging, waves per SIMD, grid, block, dynamic LDS, work-items, samples per work-item)."""
         info = rt_launch_info()
         _check(lib().rt_last_launch(self._h, C.byref(info)), "rt_last_launch")
-        return {k: getattr(info, k) for k, _ in rt_launch_info._fields_ if k != "_pad"}
+        return {k: getattr(info, k) for k, _ in rt_launch_info._fields_}
 
     def last_kernel_ms(self) -> float:
         ms = C.c_double(0)

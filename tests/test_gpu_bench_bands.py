@@ -81,6 +81,8 @@ def test_bench_frame_band_matches_oracle(gpu_ctx, key):
           f"max |d| {dmax:.3g}, NaN channels {nan_o.mean():.4f}, kernel {kms:.1f} ms, launch {launch}")
     if key.startswith("c5"):  # the 100k-sphere tree does not fit LDS: the global-memory 4-wide kernel
         assert launch["loop"] == 2 and not launch["lds_staged"] and launch["variant"] == 256 and launch["waves"] == 3
+    if key.startswith("c4"):  # media + frames: the replacement loop's mixed walk over 4-wide subtrees
+        assert launch["loop"] == 1 and launch["variant"] & 1024 and launch["wide_nodes"] > 0
     print(f"{key}: NaN masks differ in {int((nan_g != nan_o).sum())} channels")  # (counted in `ok` below)
     assert ok >= 0.999, f"{key}: only {ok:.5f} of channels within 1e-3 (max |d| {dmax:.3g})"
     assert eq >= 0.999, f"{key}: only {eq:.5f} of bytes equal"
