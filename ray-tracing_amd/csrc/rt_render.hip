@@ -400,7 +400,8 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   const char* stop_env = std::getenv("RTAMD_TRAV_STOP");
   // refill when at most trav_stop/64 of a wave's live lanes still walk (measured: C2 flat at 2-8,
   // -4 % at 16; the 100k-sphere C5 tree, walks ~3x longer, best at 16)
-  // (the full variant's walks over the caller's tree: 16, C4 1496 vs 1567 ms at 200 spp)
+  // (the full variant's walks over the caller's tree: 16 in round 2, C4 1496 vs 1567 ms at 200 spp; with
+  // the mixed walk (round 3) 8: C4 at 100 spp 323.7 vs 326.0 ms, 24: 334.0)
   // Work-items a wave claims per atomic: one claim per batch instead of one per acquisition round
   // (RTAMD_BATCH; 1 = the lanes' exact need every time). The batch tapers as the frame runs out: a
   // wave claims at most rem / (16 * waves) items when about `rem` remain, so the waves' unstarted
@@ -412,7 +413,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
     A.batch_per_item = (float)(1.0 / (16.0 * waves));
   }
   A.trav_stop = stop_env ? std::max(0, std::min(63, std::atoi(stop_env)))
-                         : (c->n_nodes > 20000 || is_full(variant_for(c->features)) ? 16 : 8);
+                         : (c->n_nodes > 20000 ? 16 : 8);
   const char* leaf_env = std::getenv("RTAMD_LEAF_STOP");
   // leaf steps once <= that many lanes still seek their first leaf (measured: C2 212.6 ms at 6-8/64
   // vs 219.7 at 0 and 232 without postponement; C5 (16 spp) 219.9 ms at 16/64 vs 326 at 0)

@@ -66,6 +66,12 @@ __device__ inline double turb(const rt_perlin* P, double sc, V3 p) {  // Lib.hs:
   }
   return fabs(acc);
 }
+// marbleTexture's value (Lib.hs:505-507). Not inlined, like sphere_uv: inlined into a render loop, the
+// turbulence's 56 unrolled lattice corners and sin's coefficients raise the whole loop's register
+// pressure (the full variant: 352 -> ~290 B/lane of scratch); as a call it costs only Perlin hits.
+__device__ __noinline__ double marble(const rt_perlin* P, double sc, V3 p) {
+  return 0.5 * (1.0 + sin(p.z + 10 * turb(P, sc, p)));
+}
 // textureValue (Lib.hs:496-510); checker chains are followed iteratively.
 template <unsigned F>
 __device__ inline V3 texture_value(const Scene& S, int tid, double u, double v, V3 p) {
@@ -76,10 +82,7 @@ __device__ inline V3 texture_value(const Scene& S, int tid, double u, double v, 
     t = &S.texs[odd ? t->a : t->b];
   }
   if (t->type == RT_TEX_CONSTANT) return v3(t->f[0], t->f[1], t->f[2]);
-  if (t->type == RT_TEX_PERLIN) {
-    const double m = 0.5 * (1.0 + sin(p.z + 10 * turb(&S.perlins[t->a], t->f[0], p)));  // marbleTexture
-    return scale(m, v3(1.0, 1.0, 1.0));
-  }
+  if (t->type == RT_TEX_PERLIN) return scale(marble(&S.perlins[t->a], t->f[0], p), v3(1.0, 1.0, 1.0));
   // RT_TEX_IMAGE
   if (t->a < 0) return v3(0, 1, 1);
   const rt_image im = S.images[t->a];
