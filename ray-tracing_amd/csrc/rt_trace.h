@@ -218,6 +218,12 @@ __device__ __forceinline__ bool sphere_t(V3 sc, double sr, const RayX& r, double
   else return false;
   return true;
 }
+// log for hit ConstantMedium's distance draw (Lib.hs:1074). Not inlined, like sphere_uv: the draw happens
+// inside the walk, and OCML's fp64 log coefficients held across the render loop cost the full variant
+// 304 -> 240 B/lane of scratch (C4 at 100 spp 323.5 -> 306.6 ms: the spill footprint is what
+// crowds the scene out of L2).
+__device__ __noinline__ double log_call(double x) { return log(x); }
+
 // A sphere hit's (u, v) from its outward normal (Lib.hs:1100-1104). Not inlined: OCML's fp64 atan and
 // asin bring polynomial coefficients that, inlined into a render loop, the compiler materialises once
 // for the whole loop and spills (the full variant: 560 -> ~290 B/lane of scratch); as a call they are
@@ -788,7 +794,7 @@ __device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, const rt_node
     const double ray_length = vlen(r.d);
     const double dist_inside = (rec2t - rec1t) * ray_length;
     const double rnd = g.draw();
-    const double hit_dist = n->f[0] * log(rnd);
+    const double hit_dist = n->f[0] * log_call(rnd);
     if (hit_dist > dist_inside) return;
     trav_take<F>(t, rec1t + (hit_dist / ray_length), id, kSubMedium, side, true);
   }
