@@ -245,6 +245,16 @@ def test_walks_output_identical(gpu_ctx, name, cam, monkeypatch):
     assert np.array_equal(rgb_w, rgb_f) and np.array_equal(rgb_w, rgb_n)
     assert np.array_equal(lin_w, lin_b, equal_nan=True) and np.array_equal(lin_w, lin_s, equal_nan=True)
     assert np.array_equal(lin_w, lin_f, equal_nan=True) and np.array_equal(lin_w, lin_n, equal_nan=True)
+    # media / frame worlds: the mixed walk over 4-wide subtrees == the same walk without them (read at
+    # upload: RTAMD_MIXW=0 builds no wide trees)
+    monkeypatch.delenv("RTAMD_REPLACE")
+    monkeypatch.delenv("RTAMD_BOX_FIRST")
+    monkeypatch.setenv("RTAMD_MIXW", "0")
+    gpu_ctx.upload(sc)
+    rgb_m, lin_m, _ = gpu_ctx.render(c, p, linear=True)
+    monkeypatch.delenv("RTAMD_MIXW")
+    gpu_ctx.upload(sc)
+    assert np.array_equal(rgb_w, rgb_m) and np.array_equal(lin_w, lin_m, equal_nan=True)
 
 
 def test_shard_invariance(gpu_ctx):
