@@ -419,8 +419,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     if (ready && t.tie && !t.redo) {  // exact tie: redo this walk as the reference does (once)
       ready = false;
       if constexpr ((F & F_COUNT) != 0) ++cnt.ties;
-      if constexpr (kRefMixed<F>) g.rewind(walk_mark);  // (the walk's media draws repeat)
-      trav_restart_ref(t, S.world_ref, INFINITY, true);
+      trav_redo<F>(t, S.world_ref, INFINITY, g, walk_mark);
       // (the redo's binary box tests need 1/d: recomputed here, the same values, so that the 4-wide
       // walk need not carry Trav::ray.inv)
       if constexpr ((F & F_WIDE) != 0) t.ray = prep(plain(t.ray));
@@ -722,8 +721,7 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
     bool walking = true;
     walk_until<F>(S, t, walking, tmin, stk, RT_BLOCK, joint != 0, 0, 0, cnt, g, side);
     if (t.tie) {
-      if (S.ref_walk) g.rewind(0);  // media draws repeat on the caller's tree
-      trav_restart_ref(t, S.world_ref, tmax, true);
+      trav_redo<F>(t, S.world_ref, tmax, g, 0u);
       while (trav_step<F>(S, t, tmin, stk, RT_BLOCK, joint != 0, cnt, g, side)) {
       }
     }

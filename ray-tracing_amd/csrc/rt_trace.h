@@ -599,6 +599,8 @@ struct Trav {
   bool ref;           // the reference's own walk: caller's tree, left first, bound = closest
   bool redo;          // a tie redo: reference semantics on every node (no RT_SUB subtrees, left
                       // child first even under RT_BVH_ORDERED nodes), so it never flags a tie
+  bool lite;          // a tie redo that only picks among the leaves hit at the tied t (trav_redo):
+                      // media are not tested
   // F_WIDE: the ray in fp32 for the conservative child-box test (wide_keys2)
   float o32x, o32y, o32z, i32x, i32y, i32z;
   float slack, tmin32, tmax32;  // slack = +inf: the fp32 distances say nothing, accept every child
@@ -679,6 +681,7 @@ __device__ __forceinline__ void trav_begin(Trav& t, const Ray& r, int root, doub
   t.tie = false;
   t.ref = false;
   t.redo = false;
+  t.lite = false;
   if constexpr ((F & F_WIDE) != 0) t.node = 0;  // wide root
   if constexpr (kRay32<F>) {
     set_ray32(t, t_min);
@@ -711,7 +714,36 @@ __device__ __forceinline__ void trav_restart_ref(Trav& t, int root, double t_max
   t.tie = false;
   t.ref = true;
   t.redo = redo;
+  t.lite = false;
   t.tmax32 = f32_upper(t_max);  // (mixed walks: the wide subtrees' bound)
+}
+
+// A walk that flagged an exact tie at t* = closest is redone as the reference does it, to pick the leaf
+// the reference's order picks among those hit at exactly t*. Its media draws need no repeat: media lie
+// only in the skeleton, which the first walk took in the reference's order under the same bounds (a
+// tie changes which leaf holds the closest t, never its value), so the draws were the reference's. The
+// redo therefore skips media (`lite`) and starts bounded by nextafter(t*): a box test at that bound
+// gives the outcome it gives at any larger bound for every box the ray enters by t*, and what it culls
+// holds no leaf hit at t*; the first leaf hit at t* is accepted as under the reference's larger bound,
+// and from then on the bound is t* itself, as in the reference. A walk whose closest hit is a medium
+// draw (a tie there needs a surface at exactly that random t) is redone in full, its draws rewound.
+// (Kernels for media-free worlds, where ties are rare — C2 none, C3 0.015 per sample — redo in full:
+// the lighter redo's extra state cost the 4-wave spheres kernel 3.5 %.)
+template <unsigned F, class R>
+__device__ __forceinline__ void trav_redo(Trav& t, int root, double t_max, R& g, uint32_t walk_mark) {
+  if constexpr (!kRefMixed<F>) {
+    trav_restart_ref(t, root, t_max, true);
+    return;
+  }
+  if (t.best_sub == kSubMedium) {
+    g.rewind(walk_mark);
+    trav_restart_ref(t, root, t_max, true);
+    return;
+  }
+  const double c = t.closest;
+  const double up = __longlong_as_double(__double_as_longlong(c) + (c > 0 ? 1 : -1));
+  trav_restart_ref(t, root, up < t_max ? up : t_max, true);  // (t* == t_max: the reference's own bound)
+  t.lite = true;
 }
 
 // Leaf of the resumable walk (a primitive, or an instance chain ending in one). Leaves are tested
@@ -755,6 +787,7 @@ __device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, const rt_node
   const int type = n->type & RT_TYPE_MASK;
   const bool chain = (F & F_INST) && (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE);
   const bool medium = (F & F_MEDIA) && type == RT_NODE_CONSTANT_MEDIUM;  // (always on the skeleton: refsem)
+  if (kRefMixed<F> && medium && t.lite) return;  // (a tie redo picks among surfaces at the tied t: trav_redo)
   if constexpr ((F & F_COUNT) != 0) {
     if (chain || medium) ++cnt.other;
     else ++cnt.prim;
