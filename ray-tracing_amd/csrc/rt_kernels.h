@@ -68,6 +68,7 @@ struct RenderArgs {
   int trav_stop;             // replacement loop: keep stepping while > trav_stop/64 of live lanes walk
   int batch;                 // replacement loop: most work-items a wave claims per atomic
   float batch_per_item;      // ...tapering to rem * batch_per_item as `rem` items remain (>= need)
+  int batch_floor;           // ...but never below this many (RTAMD_BATCH_FLOOR; 0: the lanes' need)
   int leaf_stop;             // 4-wide walk: leaf step once <= leaf_stop/64 of live lanes seek a leaf
   int box_first;             // binary walk: box-only steps while > box_first/64 of live lanes are at BVH
                              // nodes (64: never)
@@ -469,7 +470,8 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
             // roughly how many remain), so that no wave hoards the tail; never less than the need
             const uint32_t want = n_need - avail;
             const long long rem = A.work_total - (long long)q_end;
-            const uint32_t b = rem <= 0 ? 0u : (uint32_t)fminf((float)A.batch, (float)rem * A.batch_per_item);
+            const uint32_t b = rem <= 0 ? 0u : max((uint32_t)A.batch_floor,
+                                                   (uint32_t)fminf((float)A.batch, (float)rem * A.batch_per_item));
             const uint32_t got = want < b ? b : want;
             const unsigned long long c0 = atomicAdd(A.counter, (unsigned long long)got);
             // (claims past 2^32 only happen once every item is handed out: clamp, the lanes see
