@@ -72,6 +72,7 @@ struct RenderArgs {
   int leaf_stop;             // 4-wide walk: leaf step once <= leaf_stop/64 of live lanes seek a leaf
   int box_first;             // binary walk: box-only steps while > box_first/64 of live lanes are at BVH
                              // nodes (64: never)
+  uint32_t rev_tiles;        // RTAMD_TILE_REV: the slab's tiles run last to first (this count; 0: in order)
   uint8_t* out_rgb;  // tier B: slab; tier A: image
   double* out_lin;
   uint64_t* gens;  // tier A: per-column (seed, gamma), updated in place
@@ -100,8 +101,9 @@ __device__ __forceinline__ bool work_pixel(const RenderArgs& A, uint32_t w, int&
 __device__ __forceinline__ bool work_item(const RenderArgs& A, uint32_t wi, int& px, int& row, int& s0, int& s1,
                                           long long& slot) {
   const uint32_t tp = (uint32_t)(A.tile * A.tile);
-  const uint32_t lt = udiv(wi, A.div_tile);  // by tp * chunks
-  const uint32_t rem = wi - lt * tp * (uint32_t)A.chunks;
+  const uint32_t lw = udiv(wi, A.div_tile);  // by tp * chunks
+  const uint32_t rem = wi - lw * tp * (uint32_t)A.chunks;
+  const uint32_t lt = A.rev_tiles ? A.rev_tiles - 1 - lw : lw;
   const uint32_t k = udiv(rem, A.div_tp);
   const uint32_t idx = lt * tp + (rem - k * tp);
   if (!work_pixel(A, idx, px, row)) return false;

@@ -431,6 +431,8 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   // 48 416, 32 406, 16 398, 8 413; C3's Cornell kernel does not take it)
   const char* box_env = std::getenv("RTAMD_BOX_FIRST");
   A.box_first = box_env ? std::max(0, std::min(64, std::atoi(box_env))) : 16;
+  // work order only (the chunk sums do not depend on it): the slab's tiles last to first
+  A.rev_tiles = env_off("RTAMD_TILE_REV") || !std::getenv("RTAMD_TILE_REV") ? 0u : (uint32_t)per_shard;
   const unsigned var = variant_for(c->features);
   const bool count = d_work != nullptr;
   // Replacement loop (RTAMD_REPLACE=0 disables) for every world whose instance frames nest at most

@@ -344,7 +344,7 @@ def test_skewed_spine_world_walks(gpu_ctx, wide, monkeypatch):
 def test_work_claims_do_not_change_the_image(gpu_ctx, name, cam, monkeypatch):
     """Work-items are claimed per wave in batches (RTAMD_BATCH, default 1024, tapering as the frame
     runs out): which lane renders which (pixel, chunk) changes, the chunk sums and their order do
-    not, so the image is identical for any batch size. Every item must be rendered exactly once:
+    not, so the image is identical for any batch size or tile order. Every item must be rendered exactly once:
     each render follows one with another seed (a dropped item would leave that render's chunk sum
     in the buffer), and the counting build counts every sample."""
     earth = np.load(_earth_path())["rgb"] if name == "next_week_final" else None
@@ -354,8 +354,9 @@ def test_work_claims_do_not_change_the_image(gpu_ctx, name, cam, monkeypatch):
     p = rtamd.make_params(128, 96, 24, 50, rtamd.RT_RNG_PHILOX, seed=17)
     other = rtamd.make_params(128, 96, 24, 50, rtamd.RT_RNG_PHILOX, seed=99)
     out = []
-    for b in ("1", "7", "256", "4096"):
+    for b, rev in (("1", "0"), ("7", "0"), ("256", "0"), ("4096", "0"), ("256", "1")):
         monkeypatch.setenv("RTAMD_BATCH", b)
+        monkeypatch.setenv("RTAMD_TILE_REV", rev)  # the slab's tiles last to first: work order only
         gpu_ctx.render(c, other)
         out.append(gpu_ctx.render(c, p, linear=True))
         assert gpu_ctx.render_work(c, p)["samples"] == 128 * 96 * 24
