@@ -6,8 +6,9 @@ depth 50. One step = one full frame rendered by the HIP kernel (tier B Philox st
 image tiles dealt round-robin over the N ranks, slabs all-gathered over RCCL and assembled on
 rank 0. Scene and camera are resident in HBM before the timed region.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c5] [--nan-cull]
-    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU)
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1..c5] [--nan-cull]
+        (N > 1: bench.py starts the N ranks itself, one process per GPU, RCCL world N)
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU; --gpus must equal N)
 """
 import argparse
 import json
@@ -205,6 +206,70 @@ def cpu_threads(args):
     return n, {"affinity": aff, "nproc": os.cpu_count(), "omp_env": env}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_plan(gpus, env):
+    """What this process is, from --gpus and its environment (no GPU touched):
+    ("single", None) N = 1 and no launcher; ("rank", None) one rank of a launched world whose size
+    matches --gpus; ("spawn", [env, ...]) N > 1 without a launcher: the per-rank environments of the N
+    worker processes to start (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*; one GPU per rank). Raises
+    ValueError when a launcher's WORLD_SIZE disagrees with --gpus."""
+    if gpus < 1:
+        raise ValueError(f"--gpus must be >= 1, got {gpus}")
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            raise ValueError(f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks")
+        return ("rank" if world > 1 else "single"), None
+    if gpus == 1:
+        return "single", None
+    port = env.get("MASTER_PORT") or str(_free_port())
+    envs = []
+    for r in range(gpus):
+        e = dict(env)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        envs.append(e)
+    return "spawn", envs
+
+
+def spawn_ranks(cmd, envs, poll_s=0.5):
+    """Start one worker process per environment (the parent never touches the GPU), wait for all, and
+    return the first non-zero exit code (0 when every rank succeeded). When a rank fails, the others
+    are terminated (by their own PIDs) so that a barrier cannot hang the job."""
+    import subprocess
+    procs = [subprocess.Popen(cmd, env=e) for e in envs]
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    log(f"[launcher] rank {procs.index(p)} exited with {code}; stopping the others")
+                    for q in live:
+                        q.terminate()
+            if live:
+                time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -230,6 +295,16 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI, default) or gloo (rehearsal: host-staged gather)")
     args = ap.parse_args()
+
+    # --gpus N without a launcher: start N ranks (one process per GPU) before anything touches the GPU
+    try:
+        kind, envs = launch_plan(args.gpus, os.environ)
+    except ValueError as e:
+        log(f"bench.py: {e}")
+        sys.exit(2)
+    if kind == "spawn":
+        log(f"[launcher] starting {args.gpus} ranks (backend {args.dist_backend}, port {envs[0]['MASTER_PORT']})")
+        sys.exit(spawn_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], envs))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
