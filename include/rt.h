@@ -333,6 +333,24 @@ int rt_rebuild_bvh(const rt_scene_desc* desc, rt_node* out_nodes, int capacity, 
  * = the walk's stack bound (entries). RT_E_UNSUPPORTED when the root is not a BVH node. */
 int rt_wide_bvh(const rt_node* nodes, int n_nodes, int root, void* out, int capacity, int* out_n,
                 int* out_stack_need);
+/* The host half of rt_upload_scene, with no device: validates `desc` exactly as the upload does
+ * (same error codes and rt_last_error text; RT_UPLOAD_REFERENCE_BVH as for the upload) and describes
+ * the device copy it would upload. Malformed descriptors can be checked on a machine without a GPU. */
+typedef struct rt_scene_info {
+    int32_t n_nodes;         /* device node records (the caller's + the rebuilt tree) */
+    int32_t n_wide_nodes;    /* 4-wide nodes (the world's, or the mixed walk's subtrees'; 0 = none) */
+    int32_t n_leaves;        /* their leaf-table records */
+    int32_t world_root;      /* the walked world tree's root (the rebuilt one's when rebuilt) */
+    int32_t stack_need;      /* stack entries of the binary / mixed walk */
+    int32_t wide_stack_need; /* stack entries of the 4-wide walk */
+    uint32_t features;       /* scene feature bits (F_* in ray-tracing_amd/csrc/rt_layout.h) */
+    uint32_t variant;        /* the render-kernel variant chosen for them */
+    int32_t rebuilt_bvh;     /* the world tree was rebuilt (SAH, or skeleton + re-bounded subtrees) */
+    int32_t mixed_wide;      /* media / frame world with 4-wide trees under its skeleton */
+    int32_t replace_ok;      /* frames nest <= 4 deep: the ray-replacement loop applies */
+    int32_t ref_walk;        /* media or frames: walked in the reference's order */
+} rt_scene_info;
+int rt_prepare_scene(const rt_scene_desc* desc, uint32_t flags, rt_scene_info* out);
 /* Stack entries the binary walk over the tree at `root` needs (the bound rt_upload_scene sizes
  * the LDS stacks with): left-first for the caller's nodes, either child first for rebuilt
  * (RT_BVH_ORDERED) nodes, one entry per open instance frame. */

@@ -9,29 +9,9 @@
 #include <stdint.h>
 
 #include "rt.h"
+#include "rt_layout.h"
 #include "rt_wide.h"
 
-#ifndef RT_BLOCK
-#define RT_BLOCK 128 /* threads per workgroup (2 waves) */
-#endif
-#ifndef RT_STACK
-#define RT_STACK 32 /* traversal stack entries per lane (LDS) */
-#endif
-#ifndef RT_WSTACK
-#define RT_WSTACK 48 /* the same for the 4-wide walk (up to 3 siblings stacked per level) */
-#endif
-#define RT_LIGHT_DEPTH 2  /* max BVH depth of the lights tree (host-validated) */
-#define RT_MAX_FRAMES 4   /* max nesting of instance frames on the replacement loop (host-validated) */
-#define RT_FRAME 0x40000000 /* stack-entry tag: instance frame marker */
-#define RT_WNODE 0x10000000 /* node-id tag (mixed walks, F_MIXW): a 4-wide node of a re-bounded subtree */
-#define RT_ISBOX 0x08000000 /* node-id tag: a BVH node (set by the upload on the device copy's BVH children
-                               and on the roots), so that a walk schedules box steps without a load */
-#define RT_WROOT 0x20000000 /* rt_node.c flag of an RT_BVH_ORDERED node whose subtree has a 4-wide tree, */
-#define RT_WROOT_MASK 0x3ffffff /* whose root index is (c >> 2) & RT_WROOT_MASK (mixed walks) */
-#define RT_SUB 0x20000000   /* node-id tag (walks in the reference's order): inside a re-bounded,
-                               media-free subtree (below an RT_BVH_ORDERED node) */
-#define RT_CHAIN_PRIM 0x100 /* device node type flag: Translate/Rotate chain ending in a primitive */
-#define RT_TYPE_MASK 0xff
 
 namespace rtd {
 
@@ -122,15 +102,6 @@ struct Hit {
   int mat;
 };
 __device__ __forceinline__ V3 at(const Ray& r, double t) { return r.o + scale(t, r.d); }  // Lib.hs:317-318
-
-// Device material: the rt_material record plus whether its texture tree reads (u, v).
-struct DMat {
-  int type;
-  int tex;
-  double param;
-  int needs_uv;
-  int _pad;
-};
 
 struct Scene {
   const rt_node* nodes;

@@ -157,47 +157,6 @@ __device__ __forceinline__ void store_pixel(const RenderArgs& A, long long idx, 
   }
 }
 
-// One path segment: closest hit, then emission/background or a scatter. Returns true when the
-// path ends, with its contribution in `contrib` (rayColor, Lib.hs:1298-1333).
-template <unsigned F, class R>
-__device__ __forceinline__ bool segment(const RenderArgs& A, const Scene& S, Ray& ray, V3& thr, int& depth, R& g,
-                                        int* stk, V3& contrib, Cnt& cnt, int stride = RT_BLOCK,
-                                        unsigned long long* t_trav = nullptr) {
-  if (depth <= 0) {  // d <= 0 -> black
-    contrib = vmul(thr, v3(0.0, 0.0, 0.0));
-    return true;
-  }
-  Hit h;
-  // (worlds walked in the reference's order: the recursive walk takes the caller's tree as is)
-  const bool got = traverse<F>(S, S.ref_walk ? S.world_ref : S.world, ray, kEps, INFINITY, h, g, stk,
-                               !(A.flags & RT_FLAG_REFERENCE_CULL), cnt, stride);
-  if constexpr ((F & F_COUNT) != 0) *t_trav = stamp();
-  if (!got) {
-    contrib = vmul(thr, v3(S.bg[0], S.bg[1], S.bg[2]));
-    return true;
-  }
-  const DMat m = S.mats[h.mat];
-  const V3 tx = hit_texture<F>(S, m, h);
-  if (m.type == RT_MAT_DIFFUSE_LIGHT) {  // scatter -> Nothing: emitted (Lib.hs:880-885)
-    contrib = vmul(thr, h.ff ? v3(0, 0, 0) : mat_texture<F>(S, m, h, tx));
-    return true;
-  }
-  Scatter s;
-  if constexpr ((F & F_COUNT) != 0) cnt.light += (m.type == RT_MAT_LAMBERTIAN && S.lights >= 0);
-  scatter<F>(S, m, ray, h, g, s, tx);
-  if (s.specular) {
-    thr = vmul(thr, s.att);
-  } else {
-    const double c = dot(h.n, s.ray.d);  // scatteringPdf (Lib.hs:874-878)
-    const double spdf = c < 0 ? 0 : c / kPi;
-    const double k = spdf / s.pdf;
-    thr = vmul(thr, scale(k, s.att));
-  }
-  ray = s.ray;
-  --depth;
-  return false;
-}
-
 // The rest of a segment once its closest hit is known (rayColor, Lib.hs:1309-1333): background,
 // emission, or a scatter. Returns true when the path ends (contribution in `contrib`).
 template <unsigned F, class R>
@@ -227,6 +186,24 @@ __device__ __forceinline__ bool shade_hit(const Scene& S, bool got, const Hit& h
   ray = s.ray;
   --depth;
   return false;
+}
+
+// One path segment: closest hit, then emission/background or a scatter. Returns true when the
+// path ends, with its contribution in `contrib` (rayColor, Lib.hs:1298-1333).
+template <unsigned F, class R>
+__device__ __forceinline__ bool segment(const RenderArgs& A, const Scene& S, Ray& ray, V3& thr, int& depth, R& g,
+                                        int* stk, V3& contrib, Cnt& cnt, int stride = RT_BLOCK,
+                                        unsigned long long* t_trav = nullptr) {
+  if (depth <= 0) {  // d <= 0 -> black
+    contrib = vmul(thr, v3(0.0, 0.0, 0.0));
+    return true;
+  }
+  Hit h;
+  // (worlds walked in the reference's order: the recursive walk takes the caller's tree as is)
+  const bool got = traverse<F>(S, S.ref_walk ? S.world_ref : S.world, ray, kEps, INFINITY, h, g, stk,
+                               !(A.flags & RT_FLAG_REFERENCE_CULL), cnt, stride);
+  if constexpr ((F & F_COUNT) != 0) *t_trav = stamp();
+  return shade_hit<F>(S, got, h, ray, thr, depth, g, contrib, cnt);
 }
 
 // ---------------------------------------------------------------- tier B: Philox per (pixel, sample)
@@ -825,20 +802,6 @@ __global__ void math_probe(int op, const double* x, const double* y, int n, doub
 }
 
 
-// Kernel variants: spheres-only (configs 1, 2, 5), Cornell-like (rects, instances, lights), full.
-constexpr unsigned kVarSpheres = 0u;
-constexpr unsigned kVarCornell = F_RECT | F_INST | F_LIGHTS;
-// the full variant without light sampling (lights Unhittable: next_week_final, the textured
-// scenes), whose Lambertian scatter needs no lights-tree code
-constexpr unsigned kVarFullDark = (F_ALL & ~F_LIGHTS) | F_MIXW;
-// the full variant with light sampling
-constexpr unsigned kVarFull = F_ALL | F_MIXW;
-unsigned variant_for(unsigned f) {
-  if ((f & ~kVarSpheres) == 0) return kVarSpheres;
-  if ((f & ~kVarCornell) == 0) return kVarCornell;
-  return (f & F_LIGHTS) ? kVarFull : kVarFullDark;
-}
-bool is_full(unsigned var) { return (var & F_FRAMES) != 0; }
 
 // Kernel pointer for (variant, loop, LDS-staged?, waves per SIMD, counting build?); loop 0 = one
 // sample per lane walk, 1 = ray replacement over the binary tree, 2 = replacement over the

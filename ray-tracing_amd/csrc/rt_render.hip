@@ -18,14 +18,8 @@
 //  * tier B (Philox per (pixel, sample)) shards by tiles with no data-path collective; tier A
 //    (the reference's per-column SplitMix stream) runs one lane per column.
 #include "rt_kernels.h"
+#include "rt_prepare.h"
 
-#include <functional>
-
-namespace rt {
-int rebuild_world_bvh(std::vector<rt_node>& nodes, int root);
-int rebuild_for_device(std::vector<rt_node>& nodes, int root);
-bool build_wide_bvh(const std::vector<rt_node>& nodes, int root, std::vector<rt_wnode>& out, int* stack_need);
-}
 
 // =================================================================== host side
 struct rt_ctx {
@@ -48,6 +42,7 @@ struct rt_ctx {
   Scene scene{};
   unsigned features = 0;
   int n_nodes = 0;
+  int n_materials = 0, n_textures = 0;  // (rt_debug_probe checks record ids against them)
   int stack_need = 0;  // deepest traversal stack the world tree needs (entries)
   rt_wnode* d_wnodes = nullptr;  // 4-wide world tree (replace_ok worlds with a BVH root)
   rt_node* d_leaves = nullptr;   // its leaf table (Scene::leaves)
@@ -139,118 +134,6 @@ void free_scene(rt_ctx* c) {
   c->has_scene = false;
 }
 
-bool is_leaf_prim(int type) {
-  return type == RT_NODE_SPHERE || type == RT_NODE_MOVING_SPHERE || type == RT_NODE_CUBOID ||
-         (type >= RT_NODE_RECT_XY && type <= RT_NODE_RECT_YZ);
-}
-
-struct Validator {
-  const rt_scene_desc* d;
-  std::vector<rt_node> nodes;  // device copy (type flags added)
-  std::vector<int> stack_need, chain_prim, frame_depth;  // frame_depth: nesting of instance frames
-  std::string err;
-
-  bool child_ok(int parent, int child) { return child >= 0 && child < parent; }
-
-  bool run() {
-    const int n = d->n_nodes;
-    if (n <= 0 || !d->nodes) return fail("scene has no nodes");
-    nodes.assign(d->nodes, d->nodes + n);
-    stack_need.assign(n, 0);
-    chain_prim.assign(n, 0);
-    frame_depth.assign(n, 0);
-    for (int i = 0; i < n; ++i) {
-      rt_node& x = nodes[i];
-      const int t = x.type;
-      switch (t) {
-        case RT_NODE_BVH:
-          if (!child_ok(i, x.a) || !child_ok(i, x.b)) return fail("BVH child must precede its parent");
-          if (x.c <= 0) return fail("BVH size must be positive");
-          stack_need[i] = rt::bvh_stack_need(x, stack_need[x.a], stack_need[x.b]);
-          frame_depth[i] = std::max(frame_depth[x.a], frame_depth[x.b]);
-          break;
-        case RT_NODE_SPHERE:
-        case RT_NODE_RECT_XY:
-        case RT_NODE_RECT_XZ:
-        case RT_NODE_RECT_YZ:
-        case RT_NODE_CUBOID:
-          if (x.a < 0 || x.a >= d->n_materials) return fail("primitive material out of range");
-          chain_prim[i] = 1;
-          break;
-        case RT_NODE_MOVING_SPHERE:
-          if (x.a < 0 || x.a >= d->n_materials) return fail("primitive material out of range");
-          if (i + 1 >= n || d->nodes[i + 1].type != RT_NODE_EXT) return fail("MovingSphere needs its EXT record");
-          chain_prim[i] = 1;
-          break;
-        case RT_NODE_TRANSLATE:
-        case RT_NODE_ROTATE:
-          if (!child_ok(i, x.a)) return fail("instance child must precede its parent");
-          if (t == RT_NODE_ROTATE && (x.b < 0 || x.b > 2)) return fail("rotate axis out of range");
-          if (chain_prim[x.a]) {
-            chain_prim[i] = 1;
-            x.type |= RT_CHAIN_PRIM;
-          } else {
-            stack_need[i] = 1 + stack_need[x.a];
-            frame_depth[i] = 1 + frame_depth[x.a];
-          }
-          break;
-        case RT_NODE_CONSTANT_MEDIUM:
-          if (!child_ok(i, x.a)) return fail("medium boundary must precede the medium");
-          if (!chain_prim[x.a])
-            return unsup("ConstantMedium boundary must be a primitive or a Translate/Rotate chain of one");
-          if (x.b < 0 || x.b >= d->n_materials) return fail("medium material out of range");
-          break;
-        case RT_NODE_UNHITTABLE:
-        case RT_NODE_EXT:
-          break;
-        default:
-          return fail("unknown node type");
-      }
-    }
-    if (d->world_root < 0 || d->world_root >= n) return fail("world root out of range");
-    if (stack_need[d->world_root] > RT_STACK - 2) return unsup("scene BVH too deep for the LDS traversal stack");
-    if (d->lights_root >= n) return fail("lights root out of range");
-    if (d->lights_root >= 0 && !check_lights(d->lights_root, 0)) return false;
-    return true;
-  }
-  bool has_media(int id) {
-    const rt_node& x = d->nodes[id];
-    if (x.type == RT_NODE_CONSTANT_MEDIUM) return true;
-    if (x.type == RT_NODE_BVH) return has_media(x.a) || has_media(x.b);
-    if (x.type == RT_NODE_TRANSLATE || x.type == RT_NODE_ROTATE) return has_media(x.a);
-    return false;
-  }
-  bool check_lights(int id, int depth) {
-    if (has_media(id)) return unsup("lights tree must not contain ConstantMedium");
-    if (stack_need[id] > RT_STACK - 2) return unsup("lights tree too deep");
-    const rt_node& x = d->nodes[id];
-    if (x.type == RT_NODE_BVH) {
-      if (depth >= RT_LIGHT_DEPTH) return unsup("lights BVH deeper than RT_LIGHT_DEPTH");
-      return check_lights(x.a, depth + 1) && check_lights(x.b, depth + 1);
-    }
-    return true;
-  }
-  bool fail(const char* m) {
-    err = m;
-    code = RT_E_INVALID;
-    return false;
-  }
-  bool unsup(const char* m) {
-    err = m;
-    code = RT_E_UNSUPPORTED;
-    return false;
-  }
-  int code = RT_OK;
-};
-
-bool tex_needs_uv(const rt_scene_desc* d, int tid, int guard = 0) {
-  if (tid < 0 || tid >= d->n_textures || guard > 64) return false;
-  const rt_texture& t = d->textures[tid];
-  if (t.type == RT_TEX_IMAGE) return true;
-  if (t.type == RT_TEX_CHECKER) return tex_needs_uv(d, t.a, guard + 1) || tex_needs_uv(d, t.b, guard + 1);
-  return false;
-}
-
 template <class T>
 int upload(T** dst, const T* src, size_t count) {
   if (count == 0 || !src) return RT_OK;
@@ -312,27 +195,6 @@ const void* exact_variant(unsigned f) {
     case kVarCornell: return (const void*)render_exact<kVarCornell>;
     default: return (const void*)render_exact<F_ALL>;
   }
-}
-
-unsigned scene_features(const rt_scene_desc* d) {
-  unsigned f = 0;
-  for (int i = 0; i < d->n_nodes; ++i) {
-    switch (d->nodes[i].type) {
-      case RT_NODE_BVH:
-      case RT_NODE_SPHERE: break;
-      case RT_NODE_MOVING_SPHERE: f |= F_MOVING; break;
-      case RT_NODE_TRANSLATE:
-      case RT_NODE_ROTATE: f |= F_INST; break;
-      case RT_NODE_CONSTANT_MEDIUM: f |= F_MEDIA; break;
-      default: f |= F_RECT; break;  // rects, cuboids, and anything needing the full dispatch
-    }
-  }
-  if (d->world_root >= 0 && d->world_root < d->n_nodes && d->nodes[d->world_root].type == RT_NODE_UNHITTABLE)
-    f |= F_RECT;
-  if (d->lights_root >= 0) f |= F_LIGHTS;
-  for (int i = 0; i < d->n_textures; ++i)
-    if (d->textures[i].type != RT_TEX_CONSTANT) f |= F_TEX;
-  return f;
 }
 
 int launch_combine(rt_ctx* c, const RenderArgs& A, hipStream_t st) {
@@ -565,188 +427,25 @@ void rt_destroy(rt_ctx* c) {
   delete c;
 }
 
-namespace {
-
-// Mixed walks (media / frame worlds, F_MIXW): a 4-wide fp32-box tree (rt_bvh.cpp build_wide_bvh) over
-// every re-bounded subtree (an RT_BVH_ORDERED node reached from the world root through skeleton nodes
-// or frames), all in one array with one leaf table. Wide children are tagged RT_WNODE, leaves are
-// ~slot (a leaf may be a primitive, a chain, or a frame — an instance over a BVH, opened by the binary
-// walk code); each subtree's root node gets RT_WROOT and the wide root's index in `c` (device copy).
-// The walk enters the wide tree once the root's own box test passes. `host` is the unflagged rebuilt
-// tree, `dev` its validated device copy (flags added here). Sets c->d_wnodes / d_leaves and the
-// stack bound; a tree too deep for the lane stacks keeps the binary walk (no RT_WROOT marks).
-int mixed_wide_trees(rt_ctx* c, const std::vector<rt_node>& host, const std::vector<rt_node>& flat,
-                     std::vector<rt_node>& dev, int world, int ref_need) {
-  const int n = (int)dev.size();
-  if (n >= RT_WNODE) return RT_OK;  // (ids must stay clear of the RT_WNODE tag)
-  std::vector<int> roots;
-  std::vector<char> seen(2 * (size_t)n, 0);
-  std::function<void(int, bool)> find = [&](int id, bool in_ord) {
-    if (seen[2 * (size_t)id + in_ord]) return;
-    seen[2 * (size_t)id + in_ord] = 1;
-    const rt_node& x = flat[id];
-    const int ty = x.type & RT_TYPE_MASK;
-    if (ty == RT_NODE_BVH) {
-      const bool ord = (x.c & RT_BVH_ORDERED) != 0;
-      if (ord && !in_ord) roots.push_back(id);
-      find(x.a, in_ord || ord);  // (frames inside re-bounded subtrees hold subtrees of their own)
-      find(x.b, in_ord || ord);
-    } else if ((ty == RT_NODE_TRANSLATE || ty == RT_NODE_ROTATE) && !(x.type & RT_CHAIN_PRIM)) {
-      find(x.a, false);  // a frame: its child starts a new region
-    }
-  };
-  find(world, false);
-  if (roots.empty()) return RT_OK;
-  std::vector<rt_wnode> wide;
-  std::vector<int> wroot(n, -1), wneed_root(n, 0);
-  for (int r : roots) {
-    std::vector<rt_wnode> part;
-    int need = 0;
-    if (!rt::build_wide_bvh(host, r, part, &need)) return RT_OK;
-    const int base = (int)wide.size();
-    if (base + (int)part.size() > RT_WROOT_MASK) return RT_OK;
-    for (rt_wnode& w : part)
-      for (int k = 0; k < RT_WIDE; ++k)
-        if (w.child[k] >= 0) w.child[k] = (w.child[k] + base) | RT_WNODE;
-    wide.insert(wide.end(), part.begin(), part.end());
-    wroot[r] = base;
-  }
-  // the leaf table (as for the 4-wide walk): each referenced leaf once, c = its flat id
-  std::vector<rt_node> leaves;
-  std::vector<int> slot(n, -1);
-  for (rt_wnode& w : wide)
-    for (int k = 0; k < RT_WIDE; ++k) {
-      if (w.child[k] >= 0) continue;
-      const int id = ~w.child[k];
-      if (slot[id] < 0) {
-        slot[id] = (int)leaves.size();
-        leaves.push_back(flat[id]);
-        leaves.back().c = id;
-        if ((flat[id].type & RT_TYPE_MASK) == RT_NODE_MOVING_SPHERE) leaves.push_back(flat[id + 1]);
-      }
-      w.child[k] = ~slot[id];
-    }
-  // Stack bound of the mixed walk: skeleton nodes left first, re-bounded binary nodes either child
-  // first, a frame one entry, a wide node up to 3 stacked siblings (wide_node writes 3 slots) above the
-  // deepest of its children — a wide node's leaf that is a frame opens it.
-  std::vector<int> memo(n, -1);
-  std::function<int(int)> need_of;
-  std::function<int(int)> wneed = [&](int w) {
-    int deepest = 0;
-    for (int k = 0; k < RT_WIDE; ++k) {
-      const int ch = wide[w].child[k];
-      deepest = std::max(deepest, ch >= 0 ? wneed(ch & ~RT_WNODE) : need_of(leaves[~ch].c));
-    }
-    return 3 + deepest;
-  };
-  need_of = [&](int id) -> int {
-    if (memo[id] >= 0) return memo[id];
-    const rt_node& x = flat[id];
-    const int ty = x.type & RT_TYPE_MASK;
-    int r = 0;
-    if (ty == RT_NODE_BVH) {
-      if (wroot[id] >= 0) r = wneed(wroot[id]);
-      else if (x.c & RT_BVH_ORDERED) r = 1 + std::max(need_of(x.a), need_of(x.b));
-      else r = std::max(1 + need_of(x.a), need_of(x.b));
-    } else if ((ty == RT_NODE_TRANSLATE || ty == RT_NODE_ROTATE) && !(x.type & RT_CHAIN_PRIM)) {
-      r = 1 + need_of(x.a);
-    }
-    return memo[id] = r;
-  };
-  const int need = need_of(world);
-  if (need + 2 > RT_WSTACK) return RT_OK;  // (the binary walk's bound stays)
-  for (int r : roots) dev[r].c |= RT_WROOT | (wroot[r] << 2);
-  int rc;
-  if ((rc = upload(&c->d_wnodes, wide.data(), wide.size())) || (rc = upload(&c->d_leaves, leaves.data(), leaves.size())))
-    return rc;
-  HIPCHK(hipMemcpy(c->d_nodes, dev.data(), sizeof(rt_node) * dev.size(), hipMemcpyHostToDevice));
-  c->n_wnodes = (int)wide.size();
-  c->n_leaves = (int)leaves.size();
-  c->scene.wnodes = c->d_wnodes;
-  c->scene.leaves = c->d_leaves;
-  c->stack_need = std::max(need, ref_need);
-  c->mixed_wide = true;
-  return RT_OK;
-}
-
-}  // namespace
 
 int rt_upload_scene(rt_ctx* c, const rt_scene_desc* d) { return rt_upload_scene_ex(c, d, 0u); }
 
 int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
   if (!c || !din) return invalid("null argument");
-  if (din->n_nodes <= 0 || !din->nodes || din->world_root < 0 || din->world_root >= din->n_nodes)
-    return invalid("rt_upload_scene: bad node array or world root");
+  // the host half (rt_prepare.cpp): validation, the walk's trees, the tagged device copy
+  rt::PreparedScene P;
+  int rc = rt::prepare_scene(din, flags, P);
+  if (rc) return rc;
   DEVICE_SCOPE(c->device);
-  // World-tree rebuild (rt_bvh.cpp) unless the caller or RTAMD_REFERENCE_BVH=1 asks for the
-  // reference's own makeBVH tree; never for trees holding media.
-  std::vector<rt_node> nodes(din->nodes, din->nodes + din->n_nodes);
-  rt_scene_desc dd = *din;
-  const char* env = std::getenv("RTAMD_REFERENCE_BVH");
-  const bool keep = (flags & RT_UPLOAD_REFERENCE_BVH) || (env && env[0] == '1');
-  if (!keep) {
-    // validate the original first so the rebuild only ever sees well-formed DAGs
-    Validator v0{din};
-    if (!v0.run()) {
-      rt::set_error("rt_upload_scene: " + v0.err);
-      return v0.code;
-    }
-    // Worlds without media or instance frames: a whole new tree over the same leaves (exact ties are
-    // redone on the caller's tree). Worlds walked in the reference's order (media draws, frames):
-    // the skeleton above the media stays, the media-free subtrees below it (and the trees inside
-    // frames) are re-bounded; RTAMD_SKELETON=0 keeps the caller's tree as is.
-    dd.world_root = rt::rebuild_for_device(nodes, din->world_root);
-  }
-  if ((int)nodes.size() >= RT_ISBOX) return invalid("rt_upload_scene: too many nodes (ids must stay below 2^27)");
-  dd.nodes = nodes.data();
-  dd.n_nodes = (int)nodes.size();
-  const rt_scene_desc* d = &dd;
-  Validator v{d};
-  if (!v.run()) {
-    rt::set_error("rt_upload_scene: " + v.err);
-    return v.code;
-  }
-  for (int i = 0; i < d->n_textures; ++i) {
-    const rt_texture& t = d->textures[i];
-    if (t.type == RT_TEX_CHECKER && (t.a < 0 || t.a >= i || t.b < 0 || t.b >= i))
-      return invalid("rt_upload_scene: checker children must precede the checker");
-    if (t.type == RT_TEX_PERLIN && (t.a < 0 || t.a >= d->n_perlins)) return invalid("rt_upload_scene: bad perlin id");
-    if (t.type == RT_TEX_IMAGE && t.a >= 0) {
-      if (t.a >= d->n_images) return invalid("rt_upload_scene: bad image id");
-      const rt_image& im = d->images[t.a];
-      if (im.width != t.b || im.height != t.c || im.offset < 0 ||
-          im.offset + (int64_t)im.width * im.height * 3 > d->image_pool_bytes)
-        return invalid("rt_upload_scene: image raster out of the pool");
-    }
-  }
-  std::vector<DMat> mats(d->n_materials);
-  for (int i = 0; i < d->n_materials; ++i) {
-    const rt_material& m = d->materials[i];
-    if (m.type < RT_MAT_LAMBERTIAN || m.type > RT_MAT_ISOTROPIC) return invalid("rt_upload_scene: bad material");
-    if (m.type != RT_MAT_DIELECTRIC && (m.texture < 0 || m.texture >= d->n_textures))
-      return invalid("rt_upload_scene: material texture out of range");
-    mats[i] = DMat{m.type, m.texture, m.param, m.type != RT_MAT_DIELECTRIC && tex_needs_uv(d, m.texture), 0};
-  }
-  if (d->image_pool_bytes < 0 || (d->image_pool_bytes > 0 && !d->image_pool))
-    return invalid("rt_upload_scene: image_pool is null but image_pool_bytes > 0");
   free_scene(c);
-  c->rebuilt_bvh = dd.world_root != din->world_root;
-  // BVH children that are BVH nodes carry RT_ISBOX in the device copy (every walk masks it off), so
-  // that the walks' box-first scheduling knows a node's kind without loading it
-  const std::vector<rt_node> untagged = v.nodes;  // (the mixed walk's wide trees are built from it)
-  auto is_bvh = [&](int id) { return (untagged[id].type & RT_TYPE_MASK) == RT_NODE_BVH; };
-  for (rt_node& x : v.nodes)
-    if ((x.type & RT_TYPE_MASK) == RT_NODE_BVH) {
-      if (is_bvh(x.a)) x.a |= RT_ISBOX;
-      if (is_bvh(x.b)) x.b |= RT_ISBOX;
-    }
-  int rc;
-  if ((rc = upload(&c->d_nodes, v.nodes.data(), v.nodes.size())) ||
-      (rc = upload(&c->d_mats, mats.data(), mats.size())) ||
-      (rc = upload(&c->d_texs, d->textures, (size_t)d->n_textures)) ||
-      (rc = upload(&c->d_perlins, d->perlins, (size_t)d->n_perlins)) ||
-      (rc = upload(&c->d_images, d->images, (size_t)d->n_images)) ||
-      (rc = upload(&c->d_pool, d->image_pool, (size_t)d->image_pool_bytes))) {
+  if ((rc = upload(&c->d_nodes, P.nodes.data(), P.nodes.size())) ||
+      (rc = upload(&c->d_mats, P.mats.data(), P.mats.size())) ||
+      (rc = upload(&c->d_texs, din->textures, (size_t)din->n_textures)) ||
+      (rc = upload(&c->d_perlins, din->perlins, (size_t)din->n_perlins)) ||
+      (rc = upload(&c->d_images, din->images, (size_t)din->n_images)) ||
+      (rc = upload(&c->d_pool, din->image_pool, (size_t)din->image_pool_bytes)) ||
+      (rc = upload(&c->d_wnodes, P.wnodes.data(), P.wnodes.size())) ||
+      (rc = upload(&c->d_leaves, P.leaves.data(), P.leaves.size()))) {
     free_scene(c);
     return rc;
   }
@@ -757,60 +456,24 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
   S.perlins = c->d_perlins;
   S.images = c->d_images;
   S.pool = c->d_pool;
-  S.world = d->world_root | (is_bvh(d->world_root) ? RT_ISBOX : 0);
-  S.world_ref = din->world_root | (is_bvh(din->world_root) ? RT_ISBOX : 0);
-  S.lights = d->lights_root;
-  for (int i = 0; i < 3; ++i) S.bg[i] = d->background[i];
-  c->features = scene_features(d);
-  c->n_nodes = d->n_nodes;
-  // (tie redo walks the caller's tree: size the stacks for both)
-  c->stack_need = std::max(v.stack_need[d->world_root], v.stack_need[din->world_root]);
-  // The replacement loop takes every world whose frames nest at most RT_MAX_FRAMES deep (its Side
-  // slots); worlds with media or frames walk the caller's tree in the reference's order.
-  const bool frames = v.frame_depth[d->world_root] > 0;
-  c->replace_ok = v.frame_depth[d->world_root] <= RT_MAX_FRAMES;
-  S.ref_walk = (c->features & F_MEDIA) || frames;
-  if (frames) c->features |= F_FRAMES;
-  if (c->replace_ok && !S.ref_walk) {  // 4-wide fp32-box tree over the same world tree (unflagged node copy)
-    std::vector<rt_wnode> wide;
-    int need = 0;
-    if (rt::build_wide_bvh(nodes, d->world_root, wide, &need) && need + 3 <= RT_WSTACK &&
-        (size_t)wide.size() < (size_t)INT32_MAX / 2) {
-      // The walk's leaf table: the leaves the wide tree references, each copied once (a moving
-      // sphere with its EXT record), with `c` = the flat node id; leaf references ~id become ~slot.
-      std::vector<rt_node> leaves;
-      std::vector<int> slot(v.nodes.size(), -1);
-      for (rt_wnode& w : wide)
-        for (int k = 0; k < RT_WIDE; ++k) {
-          if (w.child[k] >= 0) continue;
-          const int id = ~w.child[k];
-          if (slot[id] < 0) {
-            slot[id] = (int)leaves.size();
-            leaves.push_back(v.nodes[id]);
-            leaves.back().c = id;
-            if ((v.nodes[id].type & RT_TYPE_MASK) == RT_NODE_MOVING_SPHERE) leaves.push_back(v.nodes[id + 1]);
-          }
-          w.child[k] = ~slot[id];
-        }
-      if ((rc = upload(&c->d_wnodes, wide.data(), wide.size())) ||
-          (rc = upload(&c->d_leaves, leaves.data(), leaves.size()))) {
-        free_scene(c);
-        return rc;
-      }
-      c->n_leaves = (int)leaves.size();
-      S.leaves = c->d_leaves;
-      c->n_wnodes = (int)wide.size();
-      c->wide_stack_need = std::max(need, v.stack_need[din->world_root]);
-      S.wnodes = c->d_wnodes;
-    }
-  }
-  if (c->replace_ok && S.ref_walk && !env_off("RTAMD_MIXW")) {
-    if ((rc = mixed_wide_trees(c, nodes, untagged, v.nodes, d->world_root, v.stack_need[din->world_root]))) {
-      free_scene(c);
-      return rc;
-    }
-  }
-  if (!c->d_wnodes) S.wnodes = nullptr, S.leaves = nullptr;
+  S.wnodes = c->d_wnodes;
+  S.leaves = c->d_leaves;
+  S.world = P.world;
+  S.world_ref = P.world_ref;
+  S.lights = P.lights;
+  S.ref_walk = P.ref_walk;
+  for (int i = 0; i < 3; ++i) S.bg[i] = din->background[i];
+  c->features = P.features;
+  c->n_nodes = (int)P.nodes.size();
+  c->n_materials = din->n_materials;
+  c->n_textures = din->n_textures;
+  c->n_wnodes = (int)P.wnodes.size();
+  c->n_leaves = (int)P.leaves.size();
+  c->stack_need = P.stack_need;
+  c->wide_stack_need = P.wide_stack_need;
+  c->rebuilt_bvh = P.rebuilt_bvh;
+  c->mixed_wide = P.mixed_wide;
+  c->replace_ok = P.replace_ok;
   c->has_scene = true;
   return RT_OK;
 }
@@ -1022,6 +685,18 @@ int rt_debug_probe(rt_ctx* c, const rt_camera* cam, int op, const double* in, in
     return RT_E_STATE;
   }
   if (n == 0) return RT_OK;
+  // ids the device indexes with come from the caller: check them here (an out-of-range id would be
+  // an out-of-bounds device read, not an error)
+  auto id_ok = [](double x, int count) { return std::isfinite(x) && x >= 0 && x < count && x == std::floor(x); };
+  for (int i = 0; i < n; ++i) {
+    const double* q = in + (size_t)kProbeIn[op] * i;
+    if (op == RT_PROBE_SCATTER && !id_ok(q[17], c->n_materials))
+      return invalid("rt_debug_probe: scatter record " + std::to_string(i) + " has a material id out of range");
+    if (op == RT_PROBE_TEXTURE && !id_ok(q[0], c->n_textures))
+      return invalid("rt_debug_probe: texture record " + std::to_string(i) + " has a texture id out of range");
+  }
+  if (op == RT_PROBE_HTBL_RANDOM && c->scene.lights < 0)
+    return invalid("rt_debug_probe: the scene has no lights tree");
   DEVICE_SCOPE(c->device);
   DevBuf bin, bout;
   const size_t nin = sizeof(double) * kProbeIn[op] * (size_t)n, nout = sizeof(double) * kProbeOut[op] * (size_t)n;

@@ -4,22 +4,6 @@
 
 namespace rtd {
 
-// Scene features a kernel variant is compiled for (host picks the variant per scene).
-enum : unsigned {
-  F_RECT = 1u,    // Rect / Cuboid nodes
-  F_MOVING = 2u,  // MovingSphere
-  F_INST = 4u,    // Translate / Rotate
-  F_MEDIA = 8u,   // ConstantMedium (+ Isotropic)
-  F_LIGHTS = 16u, // a lights tree (Lambertian light sampling / pdf)
-  F_TEX = 32u,    // Checker / Perlin / Image textures (and sphere u, v)
-  F_FRAMES = 512u,  // instance frames (Translate/Rotate over a BVH) in the resumable walk
-  F_ALL = 63u | 512u,
-  F_UV = 64u,     // always compute sphere (u, v) (debug queries)
-  F_COUNT = 128u, // counting build: per-lane work counters (DESIGN.md "Roofline")
-  F_WIDE = 256u,  // resumable walk over the 4-wide fp32-box tree (rt_wide.h) instead of the binary one
-  F_MIXW = 1024u  // the mixed walk (media / frame worlds) enters 4-wide fp32-box trees built over the
-                  // re-bounded subtrees (RT_WROOT nodes) instead of walking them node by node
-};
 // fp32 ray state (Trav::o32 ...) maintained: the 4-wide walk, or the mixed walk's wide subtrees
 template <unsigned F>
 constexpr bool kRay32 = (F & (F_WIDE | F_MIXW)) != 0;
@@ -1081,15 +1065,17 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
       if (n_walk <= stop) break;
       // (box-first steps only in the full variant's kernels, whose steps mix node kinds; elsewhere the
       // node-kind read and ballots would be overhead: C3 357 ms either way)
-      constexpr bool kBoxFirst = kRefMixed<F> || (F & F_COUNT) != 0;
+      // (the counting build follows the production schedule: its step counts describe the timed kernel)
+      constexpr bool kBoxFirst = kRefMixed<F>;
       // (BVH nodes and wide nodes carry their kind in the id: RT_ISBOX, RT_WNODE; a wide node's leaf is
       // negative; the counting build also reads the other kinds)
-      const bool at_box = kBoxFirst && walking && t.node >= 0 && (t.node & (RT_ISBOX | RT_WNODE));
+      const bool box_id = walking && t.node >= 0 && (t.node & (RT_ISBOX | RT_WNODE));
+      const bool at_box = kBoxFirst && box_id;
       int ty = -1;
       if constexpr ((F & F_COUNT) != 0) {
         if (walking) {
           if ((F & F_MIXW) && t.node < 0) ty = S.leaves[~t.node].type & RT_TYPE_MASK;
-          else if (at_box) ty = RT_NODE_BVH;
+          else if (box_id) ty = RT_NODE_BVH;
           else ty = S.nodes[t.node & ~(RT_SUB | RT_ISBOX)].type & RT_TYPE_MASK;
         }
       }
@@ -1101,9 +1087,10 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
       if constexpr ((F & F_COUNT) != 0) {  // counting build: wave steps, and the node kinds each one runs
         ++cnt.islot;                        // (every lane counts a step: / 64 per wave)
         const bool inst = ty == RT_NODE_TRANSLATE || ty == RT_NODE_ROTATE;
-        cnt.lslot += (__ballot(go && at_box) != 0) + (__ballot(go && inst) != 0) +
+        const bool box = ty == RT_NODE_BVH;
+        cnt.lslot += (__ballot(go && box) != 0) + (__ballot(go && inst) != 0) +
                      (__ballot(go && ty == RT_NODE_CONSTANT_MEDIUM) != 0) +
-                     (__ballot(go && !at_box && !inst && ty != RT_NODE_CONSTANT_MEDIUM) != 0);
+                     (__ballot(go && !box && !inst && ty != RT_NODE_CONSTANT_MEDIUM) != 0);
       }
       if (go) walking = trav_step<F>(S, t, t_min, stk, stride, joint, cnt, g, side);
     }

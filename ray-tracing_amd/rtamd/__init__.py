@@ -99,6 +99,12 @@ class rt_launch_info(C.Structure):
                 ("work_items", C.c_int64), ("chunk", C.c_int32), ("wide_nodes", C.c_int32)]
 
 
+class rt_scene_info(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("n_nodes", "n_wide_nodes", "n_leaves", "world_root", "stack_need",
+                                         "wide_stack_need")] + [("features", C.c_uint32), ("variant", C.c_uint32)] + [
+        (n, C.c_int32) for n in ("rebuilt_bvh", "mixed_wide", "replace_ok", "ref_walk")]
+
+
 class rt_render_params(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_int32), ("max_depth", C.c_int32),
                 ("rng_mode", C.c_int32), ("flags", C.c_uint32), ("seed", C.c_uint64), ("tile", C.c_int32),
@@ -121,6 +127,7 @@ EXPORTED = [
     "rt_render_shard_async", "rt_assemble_async", "rt_assemble_linear_async", "rt_last_kernel_ms",
     "rt_debug_closest_hits", "rt_debug_math", "rt_render_work", "rt_upload_scene_ex", "rt_rebuild_bvh",
     "rt_wide_bvh", "rt_tree_stack_need", "rt_last_launch", "rt_write_pfm", "rt_debug_probe",
+    "rt_prepare_scene",
 ]
 
 # include/rt_wide.h: one 4-wide node (128 B)
@@ -199,6 +206,7 @@ def lib() -> C.CDLL:
             "rt_last_launch": (I, [C.c_void_p, P(rt_launch_info)]),
             "rt_write_pfm": (I, [P(D), I, I, I, C.c_char_p, C.c_size_t, P(C.c_size_t)]),
             "rt_debug_probe": (I, [C.c_void_p, P(rt_camera), I, P(D), I, U64, P(D)]),
+            "rt_prepare_scene": (I, [P(rt_scene_desc), C.c_uint32, P(rt_scene_info)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -372,6 +380,16 @@ def rebuilt_scene(scene: Scene) -> Scene:
     s = Scene(scene._builder, d)
     s._keep = (arr, scene)
     return s
+
+
+def prepare_scene(scene, reference_bvh: bool = False) -> dict:
+    """rt_prepare_scene: the host half of the upload, no device needed (validation with the upload's
+    error codes, and the device copy it would make). `scene` is a Scene or an rt_scene_desc."""
+    d = scene.desc if isinstance(scene, Scene) else scene
+    info = rt_scene_info()
+    _check(lib().rt_prepare_scene(C.byref(d), RT_UPLOAD_REFERENCE_BVH if reference_bvh else 0, C.byref(info)),
+           "rt_prepare_scene")
+    return {k: getattr(info, k) for k, _ in rt_scene_info._fields_}
 
 
 def wide_bvh(scene: Scene, root: Optional[int] = None) -> Tuple[np.ndarray, int]:
