@@ -245,7 +245,18 @@ def spawn_ranks(cmd, envs, poll_s=0.5):
     return the first non-zero exit code (0 when every rank succeeded). When a rank fails, the others
     are terminated (by their own PIDs) so that a barrier cannot hang the job."""
     import subprocess
-    procs = [subprocess.Popen(cmd, env=e) for e in envs]
+    import threading
+    # rank 0's stdout is filtered: its JSON line goes to stdout, anything else the runtime prints there
+    # (gloo's connection notices) to stderr, so that stdout carries exactly one line; other ranks -> stderr
+    procs = [subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE if r == 0 else sys.stderr, text=True)
+             for r, e in enumerate(envs)]
+
+    def forward(f):
+        for line in f:
+            (sys.stdout if line.lstrip().startswith("{") else sys.stderr).write(line)
+            sys.stdout.flush()
+    pump = threading.Thread(target=forward, args=(procs[0].stdout,), daemon=True)
+    pump.start()
     rc = 0
     try:
         live = list(procs)
@@ -267,6 +278,7 @@ def spawn_ranks(cmd, envs, poll_s=0.5):
             if p.poll() is None:
                 p.kill()
                 p.wait()
+        pump.join(timeout=10)
     return rc
 
 

@@ -69,3 +69,20 @@ def test_spawn_ranks_fails_fast_and_stops_the_others():
     rc = bench.spawn_ranks([sys.executable, "-c", code], envs, poll_s=0.05)
     assert rc == 3
     assert time.time() - t0 < 30  # rank 0 was terminated, not waited for
+
+
+def test_spawn_ranks_keeps_stdout_to_the_json_line(tmp_path):
+    """Rank 0's stdout carries only its JSON line (runtime notices go to stderr); other ranks print to
+    stderr."""
+    _, envs = bench.launch_plan(2, dict(os.environ))
+    code = ("import os; r = os.environ['RANK']; print('[Gloo] Rank', r, 'is connected'); "
+            "print('{\"rank\": ' + r + '}') if r == '0' else None")
+    script = tmp_path / "w.py"
+    script.write_text(code)
+    driver = ("import sys; sys.path.insert(0, %r); import bench, os; "
+              "_, e = bench.launch_plan(2, dict(os.environ)); sys.exit(bench.spawn_ranks([sys.executable, %r], e, 0.05))"
+              % (ROOT, str(script)))
+    r = subprocess.run([sys.executable, "-c", driver], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0
+    assert r.stdout.strip().splitlines() == ['{"rank": 0}']
+    assert r.stderr.count("[Gloo]") == 2
