@@ -173,7 +173,7 @@ def pmc_valu(args):
 def sample_chunk(pixels, spp):
     """rt_sample_chunk (include/rt.h): samples per tier-B work-item."""
     fill = (pixels * spp + (1 << 20) - 1) >> 20
-    ch = max(8, (spp + 63) // 64)
+    ch = max(8, (spp + 127) // 128)
     ch = min(ch, spp, fill)
     return max(1, ch)
 

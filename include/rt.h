@@ -181,11 +181,12 @@ typedef struct rt_camera {
 #define RT_RNG_EXACT 0
 #define RT_RNG_PHILOX 1
 #define RT_CHUNK_SAMPLES 8      /* samples per chunk, at least (short chunks: a short tail per shard) */
-#define RT_CHUNK_MAX 64          /* ...but at most this many chunks per pixel (bounds the chunk sums) */
+#define RT_CHUNK_MAX 128         /* ...but at most this many chunks per pixel (bounds the chunk sums) */
 #define RT_CHUNK_ITEMS (1 << 20) /* ...fewer samples when the frame would have fewer work-items */
-/* CH = min(spp, max(8, ceil(spp / 64)), max(1, ceil(pixels * spp / 2^20))): 8-sample chunks
-   (C2), longer ones for high spp (C3/C4 1000 spp: 16, C5 2000 spp: 32) so that a pixel has at most
-   64, and shorter ones for small frames (config 1: 200x100x10 -> 1) so that they fill the device. */
+/* CH = min(spp, max(8, ceil(spp / 128)), max(1, ceil(pixels * spp / 2^20))): 8-sample chunks
+   (C2, C3/C4 at 1000 spp), longer ones for higher spp (C5 2000 spp: 16) so that a pixel has at most
+   128, and shorter ones for small frames (config 1: 200x100x10 -> 1) so that they fill the device.
+   (Round 4: 128, was 64 — 16-sample chunks left C4 a long per-shard tail at 8 GPUs.) */
 static inline int rt_sample_chunk(int64_t pixels, int spp) {
   const int64_t fill = (pixels * (int64_t)spp + RT_CHUNK_ITEMS - 1) / RT_CHUNK_ITEMS;
   int ch = (spp + RT_CHUNK_MAX - 1) / RT_CHUNK_MAX;
@@ -400,6 +401,13 @@ int rt_assemble_linear_async(rt_ctx* ctx, const rt_render_params* p, const doubl
  */
 int rt_render_work(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* p, uint64_t out_work[16]);
 
+/* The same counting render, plus a profile of the binary / mixed walk's steps (replacement loop over
+ * worlds with media or frames, and Cornell-like worlds): out_prof[m] = wave time (s_memtime ticks)
+ * of the steps whose lanes were at the set m of node kinds, out_prof[32 + m] = their count; kinds:
+ * 1 BVH box, 2 4-wide node, 4 leaf (primitive or chain), 8 ConstantMedium, 16 instance frame. */
+int rt_render_step_profile(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* p, uint64_t out_work[16],
+                           uint64_t out_prof[64]);
+
 /* Timing of the last render launch on this ctx (HIP events on the launch stream), ms. */
 int rt_last_kernel_ms(rt_ctx* ctx, double* out_ms);
 
@@ -421,6 +429,8 @@ typedef struct rt_launch_info {
     int32_t chunk;
     int32_t wide_nodes;  /* 4-wide nodes the launched walk uses: the 4-wide world tree (loop 2), or the
                             mixed walk's trees over re-bounded subtrees (loop 1, media / frame worlds) */
+    int32_t chunk_batches; /* launches the frame's chunks were split into (chunk sums bounded per launch) */
+    int32_t _pad;
 } rt_launch_info;
 int rt_last_launch(rt_ctx* ctx, rt_launch_info* out);
 

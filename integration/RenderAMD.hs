@@ -14,16 +14,19 @@
 -- column), rows split top first, rt_destroy — is mirrored in C by tests/c/ffi_sequence.c, which
 -- tests/test_ffi_sequence.py compiles and runs (the rendering half on the GPU).
 --
--- What the reference package needs for it:
---   * src/Lib.hs export list (lines 4-51): add @Camera(..)@ (exported abstractly at line 39),
---     @Rectangle(..)@ and @RGB(..)@ (not exported), so that cameras, rectangles and output pixels
---     can be taken apart / built here;
---   * random-1.2.0's "System.Random.Internal" ('StdGen' / 'unStdGen') and splitmix-0.1's
---     "System.Random.SplitMix" ('unseedSMGen'), JuicyPixels ("Codec.Picture"), vector — all
---     already dependencies (stack.yaml:42-44, package.yaml:27-35);
---   * package.yaml: @extra-libraries: rtamd@ and @extra-lib-dirs@ pointing at
---     ray-tracing_amd/build (librtamd.so pulls the ROCm runtime, libamdhip64), and @include-dirs@
---     at include/ for the ccall header names.
+-- What the reference package needs for it (integration/reference.patch, a `patch -p1` against the
+-- reference's root; then copy this file to src/RenderAMD.hs):
+--   * src/Lib.hs export list (lines 4-51): @Camera(..)@ instead of the abstract @Camera@ (line 39),
+--     and @Rectangle(..)@ and @RGB(..)@ (not exported), so that cameras, rectangles and output
+--     pixels can be taken apart / built here;
+--   * package.yaml library dependencies (lines 25-35): add @splitmix@ — this module imports
+--     "System.Random.SplitMix" ('unseedSMGen'), and splitmix is only pinned as an extra-dep
+--     (stack.yaml:42-44), not a dependency of the library; random-1.2.0's
+--     "System.Random.Internal" ('StdGen' / 'unStdGen'), JuicyPixels ("Codec.Picture"), mtl and vector
+--     already are dependencies (package.yaml:27-35);
+--   * package.yaml library: @extra-libraries: rtamd@, @extra-lib-dirs@ at ray-tracing_amd/build
+--     (librtamd.so pulls the ROCm runtime, libamdhip64) and @include-dirs@ at include/, through a
+--     link `rtamd` to this repository's checkout.
 module RenderAMD
   ( -- * Drop-ins for runRender
     runRenderAMD

@@ -64,8 +64,10 @@ __device__ __forceinline__ double div_exact(double a, double b, double y) {
   return q;
 }
 
-// A ray plus the per-ray reciprocals the exact divisions use. `safe` = every divisor in
-// [2^-900, 2^900] and a finite origin (else all divisions take the IEEE path).
+// A ray plus the per-ray reciprocals the exact divisions use. `safe` (the division-free box test's
+// condition, box_hit) = a finite origin (|o| <= 2^900) and every direction component either zero or in
+// [2^-900, 2^900]. A zero component (the +x light direction of the Lambertian quirk, DESIGN.md §4.4,
+// is (1, 0, 0)) has inv = +-inf, and a * inv is then exactly the IEEE a / +-0 (qdiv).
 struct RayX {
   V3 o, d;
   double tm;
@@ -83,16 +85,24 @@ __device__ __forceinline__ RayX prep(const Ray& r) {
   x.inv = V3{1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z};
   x.a = r.d.x * r.d.x + r.d.y * r.d.y + r.d.z * r.d.z;
   x.inva = 1.0 / x.a;
-  x.safe = div_ok(r.d.x) & div_ok(r.d.y) & div_ok(r.d.z) & div_ok(x.a) &
+  x.safe = ((r.d.x == 0.0) | div_ok(r.d.x)) & ((r.d.y == 0.0) | div_ok(r.d.y)) & ((r.d.z == 0.0) | div_ok(r.d.z)) &
            (fabs(r.o.x) <= 0x1p900) & (fabs(r.o.y) <= 0x1p900) & (fabs(r.o.z) <= 0x1p900);
   return x;
 }
 __device__ __forceinline__ Ray plain(const RayX& x) { return Ray{x.o, x.d, x.tm}; }
-// q = a / d_axis, exactly
-__device__ __forceinline__ double divd(const RayX& r, double a, int axis) {
-  const double d = axis == 0 ? r.d.x : (axis == 1 ? r.d.y : r.d.z);
-  const double y = axis == 0 ? r.inv.x : (axis == 1 ? r.inv.y : r.inv.z);
-  return r.safe ? div_exact(a, d, y) : a / d;
+// a / d exactly, given y = RN(1/d): a zero divisor gives a * y (= the IEEE a / +-0: +-inf with the
+// sign of a xor d, NaN for a = 0 or NaN), operands and quotient in [2^-900, 2^900] the Markstein
+// quotient (div_exact), anything else the IEEE division (a rare, divergent branch).
+__device__ __forceinline__ double qdiv(double a, double d, double y) {
+  double q = a * y;
+  double r = fma(-q, d, a);
+  q = fma(r, y, q);
+  r = fma(-q, d, a);
+  q = fma(r, y, q);
+  const bool zero = d == 0.0;
+  q = zero ? a * y : q;
+  if (!(zero | (in_range(a) & in_range(d) & in_range(q)))) q = a / d;
+  return q;
 }
 struct Hit {
   double t;
@@ -119,6 +129,16 @@ struct Scene {
                   // reference's own order (media draw order, Lib.hs:971-988,1053-1080)
   double bg[3];
 };
+
+// Wave-level timestamp for the counting build's phase split (MI355X_MICROARCH.md / HIP guide
+// "In-kernel stamps": one asm statement with its own lgkmcnt wait, fenced by sched barriers).
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
 
 // ------------------------------------------------------------------ RNG
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {

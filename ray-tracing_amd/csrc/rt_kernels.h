@@ -22,16 +22,6 @@ using namespace rtd;
 
 namespace {
 
-// Wave-level timestamp for the counting build's phase split (MI355X_MICROARCH.md / HIP guide
-// "In-kernel stamps": one asm statement with its own lgkmcnt wait, fenced by sched barriers).
-__device__ __forceinline__ unsigned long long stamp() {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-
 // Unsigned 32-bit division by an invariant divisor d >= 1 (Granlund & Montgomery): with
 // l = ceil(log2 d) and m = floor(2^32 (2^l - d) / d) + 1, n / d = (t + ((n - t) >> s1)) >> s2 for
 // every 32-bit n, t = umulhi(m, n), s1 = min(l, 1), s2 = max(l - 1, 0). One multiply and a few
@@ -59,12 +49,16 @@ struct RenderArgs {
   int tile, tiles_x, tiles_total, shard_rank, shard_count;
   long long work_total;  // work-items of this shard: slab pixels x sample chunks (< 2^32)
   long long slab;        // slab pixels of this shard
-  int chunk, chunks;     // tier B: samples per chunk (rt_sample_chunk) and chunks per pixel
+  int chunk, chunks;     // tier B: samples per chunk (rt_sample_chunk) and chunks per pixel in this launch
+  int chunk_base;        // the launch's first chunk (a frame may render its chunks in batches)
+  int combine;           // combine_chunks: 1 = add to the running sums in `acc`, 2 = the last batch (store)
+  double* acc;           // running per-pixel sums between chunk batches, [slab pixel][3]
   UDiv div_tp, div_tile, div_tiles_x, div_bpr;  // by tile*tile, tile*tile*chunks, tiles_x, tile/8
   double* partial;       // tier B: chunk sums, [chunk][slab pixel][3]
   uint64_t seed;
   unsigned long long* counter;
   unsigned long long* work;  // counting build: [segments, box, prim, other, light, blocks, samples]
+  unsigned long long* prof;  // counting build, optional: the walk's step profile (Cnt::prof)
   int trav_stop;             // replacement loop: keep stepping while > trav_stop/64 of live lanes walk
   int batch;                 // replacement loop: most work-items a wave claims per atomic
   float batch_per_item;      // ...tapering to rem * batch_per_item as `rem` items remain (>= need)
@@ -107,7 +101,7 @@ __device__ __forceinline__ bool work_item(const RenderArgs& A, uint32_t wi, int&
   const uint32_t k = udiv(rem, A.div_tp);
   const uint32_t idx = lt * tp + (rem - k * tp);
   if (!work_pixel(A, idx, px, row)) return false;
-  s0 = (int)k * A.chunk;
+  s0 = (A.chunk_base + (int)k) * A.chunk;
   s1 = min(A.spp, s0 + A.chunk);
   slot = (long long)k * A.slab + idx;
   return s0 < s1;
@@ -371,6 +365,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
   Trav t;  // the segment's ray lives only here between segments (no second copy is carried)
   Side side{side_p, stride};
   Cnt cnt{};
+  if constexpr ((F & F_COUNT) != 0) cnt.prof = A.prof;
   unsigned long long segs = 0, blocks = 0, samples = 0, ph_setup = 0, ph_trav = 0, ph_shade = 0;
 
   // sample s is over: add its colour; the chunk is done after its last sample
@@ -604,18 +599,25 @@ __global__ void __launch_bounds__(WAVES * 256, WAVES)
                   wave_q[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)]);
 }
 
-// Tier B: a slab pixel's chunk sums added in chunk order, then averaged and stored (rt.h).
+// Tier B: a slab pixel's chunk sums added in chunk order, then averaged and stored (rt.h); with chunk
+// batches, each batch's chunks are added to the running sum of the batches before it.
 __global__ void __launch_bounds__(256) combine_chunks(RenderArgs A) {
   const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
   if (idx >= A.slab) return;
   int px, row;
   if (!work_pixel(A, (uint32_t)idx, px, row)) return;  // outside the image: never assembled
-  V3 acc = v3(0, 0, 0);
+  V3 acc = (A.combine & 1) ? vload(A.acc + idx * 3) : v3(0, 0, 0);
   for (int k = 0; k < A.chunks; ++k) {
     const double* q = A.partial + ((long long)k * A.slab + idx) * 3;
     acc = acc + v3(q[0], q[1], q[2]);
   }
-  store_pixel(A, idx, divide(acc, (double)A.spp));
+  if (A.combine & 2) {
+    store_pixel(A, idx, divide(acc, (double)A.spp));
+  } else {  // a batch of chunks before the last: keep the running sum
+    A.acc[idx * 3 + 0] = acc.x;
+    A.acc[idx * 3 + 1] = acc.y;
+    A.acc[idx * 3 + 2] = acc.z;
+  }
 }
 
 // ---------------------------------------------------------------- tier A: the reference's stream

@@ -54,8 +54,10 @@ struct rt_ctx {
   bool replace_ok = false;  // frames nest <= RT_MAX_FRAMES deep: the replacement loop applies
   bool has_scene = false;
   unsigned long long* d_counter = nullptr;
-  double* d_partial = nullptr;  // tier-B chunk sums (grown on demand)
+  double* d_partial = nullptr;  // tier-B chunk sums (grown on demand, at most kPartialCap)
   size_t partial_bytes = 0;
+  double* d_acc = nullptr;      // running per-pixel sums of a frame rendered in chunk batches
+  size_t acc_bytes = 0;
   double last_ms = 0.0;
   rt_launch_info last_launch{};  // rt_last_launch
 };
@@ -167,6 +169,9 @@ void geometry(const rt_render_params* p, int& tile, int& tiles_x, long long& til
   slab_pixels = per_shard * tile * tile;
 }
 
+// Most bytes of chunk sums one launch writes (2 GiB; C5 at 2000 spp: 24.9 GB of chunk sums in 13 batches)
+constexpr size_t kPartialCap = 2ull << 30;
+
 // Dynamic LDS a CU's workgroup may take: 160 KiB less the replacement loop's static per-wave work
 // queues (16 waves x 8 B).
 constexpr size_t kLdsBudget = 160 * 1024 - 16 * 8;
@@ -208,7 +213,8 @@ int launch_combine(rt_ctx* c, const RenderArgs& A, hipStream_t st) {
 }
 
 int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int rank, int shards, uint8_t* d_rgb,
-                  double* d_lin, hipStream_t st, unsigned long long* d_work = nullptr) {
+                  double* d_lin, hipStream_t st, unsigned long long* d_work = nullptr,
+                  unsigned long long* d_prof = nullptr) {
   RenderArgs A{};
   A.S = c->scene;
   A.cam = *cam;
@@ -228,37 +234,76 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   // so the image no longer follows rt.h's tier-B definition)
   if (const char* ce = std::getenv("RTAMD_CHUNK")) A.chunk = std::max(1, std::min(p->spp, std::atoi(ce)));
   A.chunks = (p->spp + A.chunk - 1) / A.chunk;
-  A.work_total = slab * A.chunks;
-  // (work-item indices are 32-bit on the device, and wave claims may run up to one batch per wave
-  // past the end: keep 2^24 of headroom)
-  if (A.work_total >= (1ll << 32) - (1ll << 24))
-    return invalid("image too large: more than 2^32 - 2^24 work-items per shard");
+  A.work_total = slab * A.chunks;  // (the whole frame's; each chunk batch's launch sets its own)
   A.div_tp = make_udiv((uint32_t)(A.tile * A.tile));
-  A.div_tile = make_udiv((uint32_t)(A.tile * A.tile * A.chunks));
   A.div_tiles_x = make_udiv((uint32_t)A.tiles_x);
   A.div_bpr = make_udiv((uint32_t)(A.tile >> 3));
   A.seed = p->seed;
   A.counter = c->d_counter;
   A.work = d_work;
+  A.prof = d_prof;
   A.out_rgb = d_rgb;
   A.out_lin = d_lin;
   // The work counter and the chunk-sum buffer are the ctx's: order this launch after the previous
   // one, whichever stream that was on (on the same stream, stream order already does).
   if (st != c->last_stream) HIPCHK(hipStreamWaitEvent(st, c->ev_done, 0));
   c->last_stream = st;
-  {  // chunk sums: [chunk][slab pixel][3] doubles, kept on the ctx and grown on demand
-    const size_t need = (size_t)A.chunks * (size_t)slab * 3 * sizeof(double);
-    if (need > c->partial_bytes) {
+  // Chunk sums: [chunk][slab pixel][3] doubles, kept on the ctx and grown on demand, at most
+  // kPartialCap bytes (RTAMD_PARTIAL_CAP overrides, for tests): a frame with more chunks renders them
+  // in batches of consecutive chunks, one launch each, and combine_chunks folds each batch into a
+  // running per-pixel sum in chunk order — the sum rt.h defines, whatever the batching.
+  const int chunks_total = A.chunks;
+  const size_t per_chunk = (size_t)slab * 3 * sizeof(double);
+  size_t cap = kPartialCap;
+  if (const char* pc = std::getenv("RTAMD_PARTIAL_CAP")) cap = (size_t)std::max(1ll, std::atoll(pc));
+  const int per_batch = (int)std::max<size_t>(1, std::min<size_t>((size_t)chunks_total, cap / per_chunk));
+  const int batches = (chunks_total + per_batch - 1) / per_batch;
+  {
+    const size_t need = (size_t)per_batch * per_chunk;
+    const size_t need_acc = batches > 1 ? per_chunk : 0;
+    if (need > c->partial_bytes || need_acc > c->acc_bytes) {
       HIPCHK(hipEventSynchronize(c->ev_done));
-      (void)hipFree(c->d_partial);
-      c->d_partial = nullptr;
-      c->partial_bytes = 0;
-      HIPCHK(hipMalloc((void**)&c->d_partial, need));
-      c->partial_bytes = need;
+      if (need > c->partial_bytes) {
+        (void)hipFree(c->d_partial);
+        c->d_partial = nullptr;
+        c->partial_bytes = 0;
+        HIPCHK(hipMalloc((void**)&c->d_partial, need));
+        c->partial_bytes = need;
+      }
+      if (need_acc > c->acc_bytes) {
+        (void)hipFree(c->d_acc);
+        c->d_acc = nullptr;
+        c->acc_bytes = 0;
+        HIPCHK(hipMalloc((void**)&c->d_acc, need_acc));
+        c->acc_bytes = need_acc;
+      }
     }
     A.partial = c->d_partial;
+    A.acc = c->d_acc;
   }
-  HIPCHK(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned long long), st));
+  // (work-item indices are 32-bit on the device, and wave claims may run up to one batch per wave
+  // past the end: keep 2^24 of headroom)
+  if (slab * per_batch >= (1ll << 32) - (1ll << 24))
+    return invalid("image too large: more than 2^32 - 2^24 work-items per shard and launch");
+  // one launch per chunk batch (stream-ordered; the events span all of them)
+  auto run = [&](const void* fn, dim3 grid, dim3 block, size_t bytes, void** args) -> int {
+    for (int k0 = 0; k0 < chunks_total; k0 += per_batch) {
+      const int nk = std::min(per_batch, chunks_total - k0);
+      A.chunk_base = k0;
+      A.chunks = nk;
+      A.work_total = slab * nk;
+      A.div_tile = make_udiv((uint32_t)(A.tile * A.tile * nk));
+      A.combine = (k0 > 0 ? 1 : 0) | (k0 + nk == chunks_total ? 2 : 0);
+      HIPCHK(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned long long), st));
+      if (k0 == 0) HIPCHK(hipEventRecord(c->ev0, st));
+      HIPCHK(hipLaunchKernel(fn, grid, block, args, bytes, st));  // (arguments are copied at launch)
+      HIPCHK(hipGetLastError());
+      if (A.combine & 2) HIPCHK(hipEventRecord(c->ev1, st));
+      const int rc = launch_combine(c, A, st);
+      if (rc) return rc;
+    }
+    return RT_OK;
+  };
   const char* stop_env = std::getenv("RTAMD_TRAV_STOP");
   // refill when at most trav_stop/64 of a wave's live lanes still walk (measured: C2 flat at 2-8,
   // -4 % at 16; the 100k-sphere C5 tree, walks ~3x longer, best at 16)
@@ -344,11 +389,8 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
       void* args[] = {&A, &n_items, (void*)&entries, &n_leaves};
       c->last_launch = rt_launch_info{var | (loop == 2 ? F_WIDE : 0u), loop, 1, n_leaves > 0, waves, c->cu_count,
                                       block, (int)bytes, A.work_total, A.chunk,
-                                      (loop == 2 || (loop == 1 && c->mixed_wide)) ? c->n_wnodes : 0};
-      HIPCHK(hipEventRecord(c->ev0, st));
-      HIPCHK(hipLaunchKernel(fn, dim3(c->cu_count), dim3(block), args, bytes, st));
-      HIPCHK(hipEventRecord(c->ev1, st));
-      return launch_combine(c, A, st);
+                                      (loop == 2 || (loop == 1 && c->mixed_wide)) ? c->n_wnodes : 0, batches, 0};
+      return run(fn, dim3(c->cu_count), dim3(block), bytes, args);
     }
   }
   const void* fn = philox_kernel(var, loop, false, count ? 1 : waves, count);
@@ -363,13 +405,9 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   const int grid = (int)std::max(1ll, std::min(want, resident));
   c->last_launch = rt_launch_info{var | (loop == 2 ? F_WIDE : 0u) | (count ? F_COUNT : 0u), loop, 0, 0,
                                   count ? 1 : waves, grid, RT_BLOCK, (int)dyn, A.work_total, A.chunk,
-                                  (loop == 2 || (loop == 1 && c->mixed_wide)) ? c->n_wnodes : 0};
-  HIPCHK(hipEventRecord(c->ev0, st));
+                                  (loop == 2 || (loop == 1 && c->mixed_wide)) ? c->n_wnodes : 0, batches, 0};
   void* args[] = {&A, &entries};
-  HIPCHK(hipLaunchKernel(fn, dim3(grid), dim3(RT_BLOCK), args, dyn, st));
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(c->ev1, st));
-  return launch_combine(c, A, st);
+  return run(fn, dim3(grid), dim3(RT_BLOCK), dyn, args);
 }
 
 }  // namespace
@@ -420,6 +458,7 @@ void rt_destroy(rt_ctx* c) {
   free_scene(c);
   (void)hipFree(c->d_counter);
   (void)hipFree(c->d_partial);
+  (void)hipFree(c->d_acc);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ev_done) (void)hipEventDestroy(c->ev_done);
@@ -600,7 +639,8 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, cons
   return RT_OK;
 }
 
-int rt_render_work(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, uint64_t out_work[16]) {
+namespace {
+int render_counting(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, uint64_t* out_work, uint64_t* out_prof) {
   if (!c || !cam || !pin || !out_work) return invalid("null argument");
   int rc = check_params(pin);
   if (rc) return rc;
@@ -617,17 +657,32 @@ int rt_render_work(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin,
   geometry(&p, tile, tiles_x, tt, ps, slab);
   DevBuf slab_buf, work;
   HIPCHK(hipMalloc(&slab_buf.p, (size_t)slab * 3));
-  HIPCHK(hipMalloc(&work.p, sizeof(unsigned long long) * 16));
+  HIPCHK(hipMalloc(&work.p, sizeof(unsigned long long) * (16 + 64)));
   unsigned long long* d_work = (unsigned long long*)work.p;
-  HIPCHK(hipMemsetAsync(d_work, 0, sizeof(unsigned long long) * 16, c->stream));
-  rc = launch_philox(c, cam, &p, p.shard_rank, shards, (uint8_t*)slab_buf.p, nullptr, c->stream, d_work);
+  HIPCHK(hipMemsetAsync(d_work, 0, sizeof(unsigned long long) * (16 + 64), c->stream));
+  rc = launch_philox(c, cam, &p, p.shard_rank, shards, (uint8_t*)slab_buf.p, nullptr, c->stream, d_work,
+                     out_prof ? d_work + 16 : nullptr);
   HIPCHK(hipStreamSynchronize(c->stream));
   if (rc) return rc;
-  unsigned long long w[16];
+  unsigned long long w[16 + 64];
   HIPCHK(hipMemcpy(w, d_work, sizeof w, hipMemcpyDeviceToHost));
   for (int i = 0; i < 16; ++i) out_work[i] = w[i];
+  if (out_prof)
+    for (int i = 0; i < 64; ++i) out_prof[i] = w[16 + i];
   return RT_OK;
 }
+}  // namespace
+
+int rt_render_work(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, uint64_t out_work[16]) {
+  return render_counting(c, cam, pin, out_work, nullptr);
+}
+
+int rt_render_step_profile(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, uint64_t out_work[16],
+                           uint64_t out_prof[64]) {
+  if (!out_prof) return invalid("null argument");
+  return render_counting(c, cam, pin, out_work, out_prof);
+}
+
 
 int rt_last_kernel_ms(rt_ctx* c, double* out_ms) {
   if (!c || !out_ms) return invalid("null argument");

@@ -14,7 +14,11 @@ struct Cnt {
   unsigned islot, lslot, oslot;  // lane slots (live lanes) of wide-node steps, leaf steps, outer iterations
   unsigned phit;                 // leaf tests that found a hit
   unsigned ties;                 // walks redone for an exact tie
+  unsigned long long* prof;      // step profile (rt_render_step_profile): wave time and count of the
+                                 // walk's steps by the set of node kinds they ran (32 bins each)
 };
+// node kinds of a walk step (the step profile's bin = the set of kinds its lanes were at)
+enum : unsigned { K_BOX = 1u, K_WIDE = 2u, K_LEAF = 4u, K_MEDIUM = 8u, K_FRAME = 16u };
 
 // ------------------------------------------------------------------ textures (Lib.hs:441-513)
 __device__ __forceinline__ int hmod256(long long a) {  // Haskell `mod` pointCount
@@ -122,25 +126,32 @@ __device__ __forceinline__ bool box_hit_exact(const double* f, const RayX& r, do
 // non-NaN, (reference per-axis test) AND (joint test) is exactly L < U with
 // L = max(t_min, min(ta,tb) over axes) and U = min(t_max, max(ta,tb) over axes), and L and U are
 // each one of the exact quotients (or t_min / t_max). For a `safe` ray (finite origin, every
-// |d| in [2^-900, 2^900] so y = RN(1/d) is normal) q' = n * y is within 2^-51 |q| + 2^-1074 of
+// non-zero |d| in [2^-900, 2^900] so y = RN(1/d) is normal) q' = n * y is within 2^-51 |q| + 2^-1074 of
 // q = RN(n / d), so L', U' are within 2^-50 (|L'| + |U'|) + 2^-1073 of L, U: outside the band
 // U' - L' in [-b, b], b = 2^-48 (|L'| + |U'|) (> 2^-1000 whenever the decision is taken), the
-// sign of U' - L' is the sign of U - L. Overflowed, NaN or banded cases fall through to the
-// exact test. Branch-free except for that (rare) fall-through.
+// sign of U' - L' is the sign of U - L. An axis with d = 0 has y = +-inf and n * y is its exact
+// quotient (+-inf): with the origin inside that slab (-inf, +inf) it does not constrain L or U, as it
+// constrains nothing in the reference's per-axis test (t0 = -inf, t1 = +inf); outside it both are +inf
+// (or both -inf), so L = +inf (or U = -inf) — and the reference's test of that axis fails (its tmin is
+// +inf, or its tmax -inf). NaN quotients (n = 0: the origin on a slab plane of a zero axis), overflowed
+// or banded cases fall through to the exact test. Branch-free except for that (rare) fall-through.
 __device__ __forceinline__ bool box_hit(const double* f, const RayX& r, double t_min, double t_max, bool joint) {
   if (!joint) return box_hit_exact(f, r, t_min, t_max, false);
   double L = t_min, U = t_max;
+  bool nan = false;
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     const double o = comp(r.o, a), y = comp(r.inv, a);
     const double ta = (f[a] - o) * y, tb = (f[a + 3] - o) * y;
+    nan |= (ta != ta) | (tb != tb);
     L = fmax(L, fmin(ta, tb));
     U = fmin(U, fmax(ta, tb));
   }
   const double band = 0x1p-48 * (fabs(L) + fabs(U));
-  const bool ok_band = band > 0x1p-1000;
-  const bool yes = r.safe & ok_band & (U - L > band);
-  const bool no = r.safe & ok_band & (L - U > band);
+  const bool ok_band = (band > 0x1p-1000) & (band < INFINITY);  // (L and U finite)
+  const bool ok = r.safe & !nan;
+  const bool yes = ok & ok_band & (U - L > band);
+  const bool no = ok & ((ok_band & (L - U > band)) | (L == INFINITY) | (U == -INFINITY));
   if (yes | no) return yes;
   return box_hit_exact(f, r, t_min, t_max, true);
 }
@@ -151,8 +162,7 @@ __device__ __forceinline__ bool rect_t(int plane, double i0, double i1, double j
                                        const RayX& r, double t_min, double t_max, double& tout) {
   const int ii = plane == 2 ? 1 : 0, jj = plane == 0 ? 1 : 2, kk = plane == 0 ? 2 : (plane == 1 ? 1 : 0);
   const double num = k - comp(r.o, kk);
-  double t = r.safe ? div_mk(num, comp(r.d, kk), comp(r.inv, kk)) : 0.0;
-  if (!r.safe || !q_ok(num, t)) t = num / comp(r.d, kk);
+  double t = qdiv(num, comp(r.d, kk), comp(r.inv, kk));
   if ((t < t_min) || (t > t_max)) return false;
   const double i = comp(r.o, ii) + t * comp(r.d, ii);
   const double j = comp(r.o, jj) + t * comp(r.d, jj);
@@ -193,7 +203,7 @@ __device__ __forceinline__ bool sphere_t(V3 sc, double sr, const RayX& r, double
   const double sd = sqrt(disc);
   const double n1 = (-b) - sd, n2 = (-b) + sd;
   double temp1 = div_mk(n1, a, r.inva), temp2 = div_mk(n2, a, r.inva);
-  if (!(r.safe & q_ok(n1, temp1) & q_ok(n2, temp2))) {
+  if (!(in_range(a) & q_ok(n1, temp1) & q_ok(n2, temp2))) {
     temp1 = n1 / a;
     temp2 = n2 / a;
   }
@@ -579,7 +589,8 @@ struct Trav {
   int pend;           // F_WIDE: a postponed leaf (flat node id), -1 = none
   int level;          // F_INST: open instance frames (their ids in the lane's Side slots)
   int best_level;     // F_INST: frames around the best hit (copied to Side::best)
-  bool tie;           // a second leaf hit at exactly `closest`: the walk is redone with `ref`
+  bool tie;           // another leaf hit at exactly `closest` whose record may shade differently (tie_same):
+                      // the walk is redone with `ref`
   bool ref;           // the reference's own walk: caller's tree, left first, bound = closest
   bool redo;          // a tie redo: reference semantics on every node (no RT_SUB subtrees, left
                       // child first even under RT_BVH_ORDERED nodes), so it never flags a tie
@@ -740,8 +751,39 @@ __device__ __forceinline__ void trav_redo(Trav& t, int root, double t_max, R& g,
 // `refsem`: the reference's own semantics for this leaf (a ref walk outside any re-bounded
 // subtree): its bound is `closest` and every accepted hit replaces, as hit BVHNode prefers the
 // right child's hit. Otherwise the bound is closest_up and an exact tie is flagged.
+// Which face of which material a plain rect / cuboid leaf's hit is on: plane (0 XY, 1 XZ, 2 YZ) and
+// material id; -1 for every other leaf (spheres, moving spheres).
+__device__ __forceinline__ int face_sig(const rt_node* n, int sub) {
+  const int type = n->type & RT_TYPE_MASK;
+  const int plane = type == RT_NODE_CUBOID ? (sub >> 1) : type - RT_NODE_RECT_XY;
+  return (type == RT_NODE_CUBOID || (type >= RT_NODE_RECT_XY && type <= RT_NODE_RECT_YZ)) ? plane | (n->a << 2) : -1;
+}
+// An exact tie needs no redo when the tied leaves' hit records shade identically: two rect faces (plain
+// rects or cuboid faces, outside instance frames) on the same plane orientation with the same material,
+// whose texture does not read (u, v). Their records then agree in t, p (the same ray at the same t),
+// outward normal, hence front_face and normal (faceNormal, Lib.hs:1111-1117), and material; u and v
+// differ but reach nothing (textureValue of a (u, v)-free texture). Whichever of them the reference's
+// order picks (Lib.hs:971-1004), the rest of the path — its draws and its colour — is the same. (Such
+// ties are what the +x light direction of the Lambertian quirk produces along the box field of
+// next_week_final: a box's +x face and its neighbour's -x face in one plane)
+// Debug kernels (F_UV) compare u, v too: there every tie is redone.
 template <unsigned F>
-__device__ __forceinline__ void trav_take(Trav& t, double x, int id, int sub, Side& side, bool refsem) {
+constexpr bool kTieSameOk = (F & F_RECT) != 0 && (F & F_UV) == 0;
+template <unsigned F>
+__device__ __forceinline__ bool tie_same(const Scene& S, const Trav& t, const rt_node* n, int sub, bool plain) {
+  if constexpr (!kTieSameOk<F>) return false;
+  int best_level = 0;
+  if constexpr ((F & F_FRAMES) != 0) best_level = t.best_level + t.level;
+  if (!plain || best_level != 0 || t.best_node < 0 || (t.best_sub & kSubChain) || t.best_sub == kSubMedium) return false;
+  const rt_node* b = ((F & (F_WIDE | F_MIXW)) && (t.best_node & kSlotTag)) ? &S.leaves[t.best_node & ~kSlotTag]
+                                                                          : &S.nodes[t.best_node];
+  const int sig = face_sig(n, sub);
+  return sig >= 0 && sig == face_sig(b, t.best_sub) && !S.mats[n->a].needs_uv;
+}
+
+template <unsigned F>
+__device__ __forceinline__ void trav_take(const Scene& S, Trav& t, double x, int id, int sub, Side& side, bool refsem,
+                                          const rt_node* leaf, bool plain) {
   if (refsem || x < t.closest) {
     // (a tie at the old closest no longer matters: only leaves hit at the final closest t compete, and
     // the bound the walk carried on with was the same whichever tied leaf won)
@@ -755,7 +797,8 @@ __device__ __forceinline__ void trav_take(Trav& t, double x, int id, int sub, Si
     }
     if constexpr (kRay32<F>) t.tmax32 = f32_upper(x);
   } else if (x == t.closest && id != t.best_node) {  // (the same leaf twice is no tie)
-    t.tie = true;
+    // (a tie whose records shade identically needs no redo: tie_same)
+    if (!tie_same<F>(S, t, leaf, sub, plain)) t.tie = true;
   }
 }
 // A leaf: a primitive, an instance chain ending in one (its t and face only: the record is built once,
@@ -812,7 +855,7 @@ __device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, const rt_node
   if (!ok) return;
   if (!medium) {
     if constexpr ((F & F_COUNT) != 0) cnt.phit += !chain;
-    trav_take<F>(t, tt, id, chain ? (kSubChain | sub) : sub, side, refsem);
+    trav_take<F>(S, t, tt, id, chain ? (kSubChain | sub) : sub, side, refsem, p, !chain);
     return;
   }
   if constexpr ((F & F_MEDIA) != 0) {  // the rest of hit ConstantMedium (Lib.hs:1062-1080)
@@ -826,7 +869,7 @@ __device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, const rt_node
     const double rnd = g.draw();
     const double hit_dist = n->f[0] * log_call(rnd);
     if (hit_dist > dist_inside) return;
-    trav_take<F>(t, rec1t + (hit_dist / ray_length), id, kSubMedium, side, true);
+    trav_take<F>(S, t, rec1t + (hit_dist / ray_length), id, kSubMedium, side, true, n, false);
   }
 }
 
@@ -1092,7 +1135,30 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
                      (__ballot(go && ty == RT_NODE_CONSTANT_MEDIUM) != 0) +
                      (__ballot(go && !box && !inst && ty != RT_NODE_CONSTANT_MEDIUM) != 0);
       }
+      unsigned kinds = 0;
+      unsigned long long t0 = 0;
+      if constexpr ((F & F_COUNT) != 0) {
+        const bool wide = walking && t.node >= 0 && (t.node & RT_WNODE);
+        const bool inst = ty == RT_NODE_TRANSLATE || ty == RT_NODE_ROTATE;
+        bool frame = false;
+        if (inst) {
+          const int nid = t.node < 0 ? -1 : (t.node & ~(RT_SUB | RT_ISBOX));
+          const int tf = t.node < 0 ? S.leaves[~t.node].type : S.nodes[nid].type;
+          frame = !(tf & RT_CHAIN_PRIM);
+        }
+        kinds = (__ballot(go && ty == RT_NODE_BVH && !wide) ? K_BOX : 0u) | (__ballot(go && wide) ? K_WIDE : 0u) |
+                (__ballot(go && ty == RT_NODE_CONSTANT_MEDIUM) ? K_MEDIUM : 0u) | (__ballot(go && frame) ? K_FRAME : 0u) |
+                (__ballot(go && ty >= 0 && ty != RT_NODE_BVH && ty != RT_NODE_CONSTANT_MEDIUM && !frame) ? K_LEAF : 0u);
+        t0 = stamp();
+      }
       if (go) walking = trav_step<F>(S, t, t_min, stk, stride, joint, cnt, g, side);
+      if constexpr ((F & F_COUNT) != 0) {
+        const unsigned long long t1 = stamp();
+        if (cnt.prof && __lane_id() == (unsigned)(__ffsll((long long)__ballot(true)) - 1)) {
+          atomicAdd(&cnt.prof[kinds], t1 - t0);
+          atomicAdd(&cnt.prof[32 + kinds], 1ull);
+        }
+      }
     }
   } else {
     for (;;) {
@@ -1126,7 +1192,7 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
 // instance frames is recorded in the innermost frame's ray, then each frame's rewrite is applied from
 // the innermost outwards with the ray its child saw (as `traverse` does when frames close); a chain's
 // instances likewise (chain_hit). `r` is the world ray. Callers check `tie` first and re-walk with
-// trav_restart_ref. One inlined copy of the record code (prim_record) per kernel.
+// trav_restart_ref (ties between shading-identical records need none: tie_same). One inlined copy of the record code (prim_record) per kernel.
 template <unsigned F>
 __device__ __forceinline__ bool trav_finish(const Scene& S, const Trav& t, const Ray& r, double t_min, Hit& h,
                                             const Side& side) {

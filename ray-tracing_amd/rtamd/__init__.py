@@ -96,7 +96,8 @@ class rt_camera(C.Structure):
 class rt_launch_info(C.Structure):
     _fields_ = [("variant", C.c_uint32), ("loop", C.c_int32), ("lds_staged", C.c_int32), ("leaf_lds", C.c_int32),
                 ("waves", C.c_int32), ("grid", C.c_int32), ("block", C.c_int32), ("dyn_lds_bytes", C.c_int32),
-                ("work_items", C.c_int64), ("chunk", C.c_int32), ("wide_nodes", C.c_int32)]
+                ("work_items", C.c_int64), ("chunk", C.c_int32), ("wide_nodes", C.c_int32),
+                ("chunk_batches", C.c_int32), ("_pad", C.c_int32)]
 
 
 class rt_scene_info(C.Structure):
@@ -127,7 +128,7 @@ EXPORTED = [
     "rt_render_shard_async", "rt_assemble_async", "rt_assemble_linear_async", "rt_last_kernel_ms",
     "rt_debug_closest_hits", "rt_debug_math", "rt_render_work", "rt_upload_scene_ex", "rt_rebuild_bvh",
     "rt_wide_bvh", "rt_tree_stack_need", "rt_last_launch", "rt_write_pfm", "rt_debug_probe",
-    "rt_prepare_scene",
+    "rt_prepare_scene", "rt_render_step_profile",
 ]
 
 # include/rt_wide.h: one 4-wide node (128 B)
@@ -207,6 +208,7 @@ def lib() -> C.CDLL:
             "rt_write_pfm": (I, [P(D), I, I, I, C.c_char_p, C.c_size_t, P(C.c_size_t)]),
             "rt_debug_probe": (I, [C.c_void_p, P(rt_camera), I, P(D), I, U64, P(D)]),
             "rt_prepare_scene": (I, [P(rt_scene_desc), C.c_uint32, P(rt_scene_info)]),
+            "rt_render_step_profile": (I, [C.c_void_p, P(rt_camera), P(rt_render_params), P(U64), P(U64)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -551,6 +553,20 @@ class Context:
         out["lane_slots"] = {"wide_steps": int(w[11]), "leaf_steps": int(w[12]), "outer_iterations": int(w[13])}
         out["leaf_hits"] = int(w[14])  # replacement loop only: leaf tests that found a hit
         out["tie_redos"] = int(w[15])  # replacement loop only: walks (or samples) redone for an exact tie
+        return out
+
+    STEP_KINDS = ("box", "wide", "leaf", "medium", "frame")
+
+    def step_profile(self, cam, params) -> dict:
+        """rt_render_step_profile: the binary / mixed walk's steps by the set of node kinds their lanes
+        were at: {"box+leaf": (ticks, steps), ...} (s_memtime ticks, counting build)."""
+        w, p = (C.c_uint64 * 16)(), (C.c_uint64 * 64)()
+        _check(lib().rt_render_step_profile(self._h, C.byref(cam), C.byref(params), w, p), "rt_render_step_profile")
+        out = {}
+        for m in range(32):
+            if p[32 + m]:
+                name = "+".join(k for i, k in enumerate(self.STEP_KINDS) if m >> i & 1) or "none"
+                out[name] = (int(p[m]), int(p[32 + m]))
         return out
 
     def last_launch(self) -> dict:

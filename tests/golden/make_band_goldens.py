@@ -12,11 +12,12 @@ exists here; they pin the HIP path against the oracle at the bench launches.
 
 Bands (key prefix: frame, rows):
   c2_  makeRandomSceneBookOne 1200x800, 500 spp, depth 50 (8-sample chunks x 63), rows 396..403
-  c3_  makeCornellBoxScene 600x600, 1000 spp, depth 50 (16-sample chunks), rows 296..303
-  c4_  makeNextWeekFinalScene + earth raster 800x800, 1000 spp, depth 50 (16-sample chunks), rows 398..399
+  c3_  makeCornellBoxScene 600x600, 1000 spp, depth 50 (8-sample chunks x 125), rows 296..303
+  c4_  makeNextWeekFinalScene + earth raster 800x800, 1000 spp, depth 50 (8-sample chunks), rows 396..403
   c5_  stress 100k spheres 3840x2160 at 4 spp, depth 50 (the global-memory 4-wide kernel), rows 1079..1080
-  c4s_ the C4 frame at 16 spp (one chunk per pixel), rows 398..401
-  c2z_, c4z_, c5z_  the C2 / C4 / C5 bands again with RT_FLAG_NAN_ZERO (include/rt.h, a parity
+  c5b_ the C5 frame at its bench spp, 2000 (16-sample chunks x 125, rendered in chunk batches), row 1080
+  c4s_ the C4 frame at 16 spp (two chunks per pixel), rows 398..401
+  c2z_, c4z_, c5z_, c5bz_  the C2 / C4 / C5 bands again with RT_FLAG_NAN_ZERO (include/rt.h, a parity
        diagnostic): the reference's Lambertian light-mixture quirk makes 99.9 % of
        the C2 band's channels and all of C4's NaN at the bench spp, so the plain bands compare little
        more than NaN masks; with the flag each sample's finite colour reaches the average, so the same
@@ -45,12 +46,14 @@ Z = rtamd.RT_FLAG_NAN_ZERO
 BANDS = [
     ("c2", "random_book_one", "random_scene", 1200, 800, 500, 50, 0, False, 396, 8, 0),
     ("c3", "cornell", "cornell", 600, 600, 1000, 50, 0, False, 296, 8, 0),
-    ("c4", "next_week_final", "next_week", 800, 800, 1000, 50, 0, True, 398, 2, 0),
+    ("c4", "next_week_final", "next_week", 800, 800, 1000, 50, 0, True, 396, 8, 0),
     ("c5", "stress_spheres", "random_scene", 3840, 2160, 4, 50, 100000, False, 1079, 2, 0),
+    ("c5b", "stress_spheres", "random_scene", 3840, 2160, 2000, 50, 100000, False, 1080, 1, 0),
     ("c4s", "next_week_final", "next_week", 800, 800, 16, 50, 0, True, 398, 4, 0),
     ("c2z", "random_book_one", "random_scene", 1200, 800, 500, 50, 0, False, 396, 8, Z),
-    ("c4z", "next_week_final", "next_week", 800, 800, 1000, 50, 0, True, 398, 2, Z),
+    ("c4z", "next_week_final", "next_week", 800, 800, 1000, 50, 0, True, 396, 8, Z),
     ("c5z", "stress_spheres", "random_scene", 3840, 2160, 4, 50, 100000, False, 1079, 2, Z),
+    ("c5bz", "stress_spheres", "random_scene", 3840, 2160, 2000, 50, 100000, False, 1080, 1, Z),
 ]
 SEED = 1024
 
@@ -82,6 +85,11 @@ def build(keys=None):
 
 
 if __name__ == "__main__":
-    g = build(sys.argv[1:])
+    keys = sys.argv[1:]
+    g = build(keys)
+    if keys and os.path.exists(OUT):  # (rebuild some bands, keep the others)
+        old = dict(np.load(OUT))
+        old.update(g)
+        g = old
     np.savez_compressed(OUT, **g)
     print(OUT, os.path.getsize(OUT), "bytes")

@@ -36,8 +36,9 @@ def test_struct_sizes_match_header():
     assert C.sizeof(rtamd.rt_node) == 64
     assert C.sizeof(rtamd.rt_scene_desc) == 112
     assert C.sizeof(rtamd.rt_render_params) == 48
-    assert C.sizeof(rtamd.rt_launch_info) == 48
+    assert C.sizeof(rtamd.rt_launch_info) == 56
     assert rtamd.rt_launch_info.wide_nodes.offset == 44  # (round 3: was _pad)
+    assert rtamd.rt_launch_info.chunk_batches.offset == 48  # (round 4)
 
 
 def test_param_validation_without_gpu():

@@ -35,3 +35,29 @@ def test_ffi_sequence_renders_gpu(exe):
     r = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=240)
     print(r.stdout, r.stderr)
     assert r.returncode == 0 and r.stdout.count("identical bytes") == 4
+
+
+def test_reference_patch_applies(tmp_path):
+    """integration/reference.patch (what the reference needs for integration/RenderAMD.hs: the Lib
+    exports, splitmix as a library dependency, the link flags) applies cleanly to the reference's
+    package.yaml and src/Lib.hs, and covers every package the module imports."""
+    ref = "/root/reference"
+    if not os.path.isdir(ref):
+        pytest.skip("the reference checkout is not present on this machine")
+    import shutil
+    os.makedirs(tmp_path / "src")
+    shutil.copy(os.path.join(ref, "package.yaml"), tmp_path / "package.yaml")
+    shutil.copy(os.path.join(ref, "src", "Lib.hs"), tmp_path / "src" / "Lib.hs")
+    patch = os.path.join(ROOT, "integration", "reference.patch")
+    r = subprocess.run(["patch", "-p1", "-i", patch], cwd=tmp_path, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    pkg = (tmp_path / "package.yaml").read_text()
+    lib = (tmp_path / "src" / "Lib.hs").read_text()
+    assert "- splitmix" in pkg and "extra-libraries: rtamd" in pkg
+    assert "Camera(..)" in lib and "Rectangle(..)" in lib and "RGB(..)" in lib
+    hs = open(os.path.join(ROOT, "integration", "RenderAMD.hs")).read()
+    imports = {"System.Random.SplitMix": "splitmix", "System.Random.Internal": "random", "Codec.Picture": "JuicyPixels",
+               "Control.Monad.State.Strict": "mtl", "Data.Vector": "vector"}
+    for mod, package in imports.items():
+        if f"import           {mod}" in hs or f"import qualified {mod}" in hs:
+            assert f"- {package}" in pkg, (mod, package)

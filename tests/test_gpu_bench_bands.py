@@ -68,7 +68,7 @@ def render_like_bench(ctx, cfg, W, H, spp, depth, seed, flags):
     return frame.image.cpu().numpy(), lin.cpu().numpy(), t["kernel_ms"], ctx.last_launch()
 
 
-@pytest.mark.parametrize("key", ["c2", "c3", "c4", "c5", "c4s", "c2z", "c4z", "c5z"])
+@pytest.mark.parametrize("key", ["c2", "c3", "c4", "c5", "c5b", "c4s", "c2z", "c4z", "c5z", "c5bz"])
 def test_bench_frame_band_matches_oracle(gpu_ctx, key):
     W, H, spp, depth, seed, r0, flags = [int(x) for x in B[f"{key}_frame"]]
     rgb_o, lin_o = B[f"{key}_rgb"], B[f"{key}_lin"]
@@ -83,6 +83,11 @@ def test_bench_frame_band_matches_oracle(gpu_ctx, key):
         assert launch["loop"] == 2 and not launch["lds_staged"] and launch["variant"] == 256 and launch["waves"] == 3
     if key.startswith("c4"):  # media + frames: the replacement loop's mixed walk over 4-wide subtrees
         assert launch["loop"] == 1 and launch["variant"] & 1024 and launch["wide_nodes"] > 0
+    # the bench frames' own chunking (rt_sample_chunk): 8-sample chunks at 500 / 1000 spp, 16 at C5's 2000
+    # spp, whose 125 chunks' sums (24.9 GB) are rendered in batches of at most 2 GiB of chunk sums
+    assert launch["chunk"] == {500: 8, 1000: 8, 2000: 16, 16: 8, 4: 4}[spp]
+    if key.startswith("c5b"):
+        assert launch["chunk_batches"] == 13
     print(f"{key}: NaN masks differ in {int((nan_g != nan_o).sum())} channels")
     assert (nan_g == nan_o).all(), f"{key}: NaN masks differ"  # (NaN comes from pdf 0, never from rounding)
     assert ok >= 0.999, f"{key}: only {ok:.5f} of channels within 1e-3 (max |d| {dmax:.3g})"

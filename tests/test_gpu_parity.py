@@ -60,10 +60,10 @@ def test_book_one_tier_b(gpu_ctx):
 
 
 @pytest.mark.parametrize("w,h,spp,ch", [(32, 24, 33, 1), (64, 64, 600, 3), (128, 96, 700, 9), (256, 256, 130, 8),
-                                        (160, 120, 1100, 18)])
+                                        (160, 120, 2200, 18)])
 def test_tier_b_sample_chunks(gpu_ctx, w, h, spp, ch):
     """A pixel's samples are summed per chunk (rt_sample_chunk: the fill-limited 1, 3, 9 and the
-    8-sample floor and ceil(spp/64) branches at 8 and 18), chunk sums in chunk order — the device's
+    8-sample floor and ceil(spp/128) branches at 8 and 18), chunk sums in chunk order — the device's
     work-items, combined by `combine_chunks` — exactly as the oracle. The last two use config 1's
     scene at depth 10 with RT_FLAG_NAN_ZERO, so that every sample's finite colour is summed (cheap
     for the oracle; the light-mixture quirk would make most pixels NaN)."""
@@ -344,7 +344,8 @@ def test_skewed_spine_world_walks(gpu_ctx, wide, monkeypatch):
 def test_work_claims_do_not_change_the_image(gpu_ctx, name, cam, monkeypatch):
     """Work-items are claimed per wave in batches (RTAMD_BATCH, default 1024, tapering as the frame
     runs out): which lane renders which (pixel, chunk) changes, the chunk sums and their order do
-    not, so the image is identical for any batch size or tile order. Every item must be rendered exactly once:
+    not, so the image is identical for any batch size, tile order or chunk batching. Every item must be
+    rendered exactly once:
     each render follows one with another seed (a dropped item would leave that render's chunk sum
     in the buffer), and the counting build counts every sample."""
     earth = np.load(_earth_path())["rgb"] if name == "next_week_final" else None
@@ -354,11 +355,20 @@ def test_work_claims_do_not_change_the_image(gpu_ctx, name, cam, monkeypatch):
     p = rtamd.make_params(128, 96, 24, 50, rtamd.RT_RNG_PHILOX, seed=17)
     other = rtamd.make_params(128, 96, 24, 50, rtamd.RT_RNG_PHILOX, seed=99)
     out = []
-    for b, rev in (("1", "0"), ("7", "0"), ("256", "0"), ("4096", "0"), ("256", "1")):
+    slab_chunk = 128 * 96 * 3 * 8  # one chunk's sums (the 24 chunks of one sample each)
+    for b, rev, cap in (("1", "0", 0), ("7", "0", 0), ("256", "0", 0), ("4096", "0", 0), ("256", "1", 0),
+                        ("256", "0", 5 * slab_chunk), ("1024", "0", 1)):
         monkeypatch.setenv("RTAMD_BATCH", b)
         monkeypatch.setenv("RTAMD_TILE_REV", rev)  # the slab's tiles last to first: work order only
+        # chunk sums bounded per launch: the chunks render in batches (5 of 5 chunks, 24 of 1), folded
+        # into running sums in chunk order
+        if cap:
+            monkeypatch.setenv("RTAMD_PARTIAL_CAP", str(cap))
+        else:
+            monkeypatch.delenv("RTAMD_PARTIAL_CAP", raising=False)
         gpu_ctx.render(c, other)
         out.append(gpu_ctx.render(c, p, linear=True))
+        assert gpu_ctx.last_launch()["chunk_batches"] == ({0: 1, 1: 24}.get(cap, 5))
         assert gpu_ctx.render_work(c, p)["samples"] == 128 * 96 * 24
     for rgb, lin, _ in out[1:]:
         assert np.array_equal(rgb, out[0][0]) and np.array_equal(lin, out[0][1], equal_nan=True)
