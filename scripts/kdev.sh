@@ -4,7 +4,7 @@
 # usage: scripts/kdev.sh '<explicit instantiation>' [--isa FILE] [extra hipcc flags...]
 #   e.g. scripts/kdev.sh 'render_philox2<559u, 3>(RenderArgs, int)' --isa /tmp/c4.s
 set -eo pipefail
-root=$(cd "$(dirname "$0")/.." && pwd)
+root=${KDEV_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}  # (KDEV_ROOT: another source tree, e.g. /tmp/ab_src_NAME)
 inst=$1; shift
 isa=""
 if [ "${1:-}" = "--isa" ]; then isa=$2; shift 2; fi

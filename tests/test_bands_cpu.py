@@ -41,7 +41,7 @@ def test_nan_zero_keeps_the_finite_part():
 
 
 def test_sample_chunk_mirror():
-    for (px, spp), ch in {(768, 33): 1, (4096, 600): 3, (12288, 700): 9, (65536, 130): 8, (19200, 1100): 9,
+    for (px, spp), ch in {(768, 33): 1, (4096, 600): 3, (12288, 700): 8, (7680, 1200): 9, (65536, 130): 8, (19200, 1100): 9,
                           (19200, 2200): 18, (960000, 500): 8, (360000, 1000): 8, (640000, 1000): 8,
                           (8294400, 2000): 16, (20000, 10): 1, (8294400, 4): 4}.items():
         assert bench.sample_chunk(px, spp) == ch

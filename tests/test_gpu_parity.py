@@ -59,7 +59,7 @@ def test_book_one_tier_b(gpu_ctx):
     _cmp(gpu_ctx, sc, cam, p)
 
 
-@pytest.mark.parametrize("w,h,spp,ch", [(32, 24, 33, 1), (64, 64, 600, 3), (128, 96, 700, 9), (256, 256, 130, 8),
+@pytest.mark.parametrize("w,h,spp,ch", [(32, 24, 33, 1), (64, 64, 600, 3), (80, 96, 1200, 9), (256, 256, 130, 8),
                                         (160, 120, 2200, 18)])
 def test_tier_b_sample_chunks(gpu_ctx, w, h, spp, ch):
     """A pixel's samples are summed per chunk (rt_sample_chunk: the fill-limited 1, 3, 9 and the
