@@ -64,17 +64,15 @@ __device__ __forceinline__ double div_exact(double a, double b, double y) {
   return q;
 }
 
-// A ray plus the per-ray reciprocals the exact divisions use. `safe` (the division-free box test's
-// condition, box_hit) = a finite origin (|o| <= 2^900) and every direction component either zero or in
-// [2^-900, 2^900]. A zero component (the +x light direction of the Lambertian quirk, DESIGN.md §4.4,
-// is (1, 0, 0)) has inv = +-inf, and a * inv is then exactly the IEEE a / +-0 (qdiv).
+// A ray plus the per-ray reciprocals the exact divisions use. A zero component (the +x light direction
+// of the Lambertian quirk, DESIGN.md §4.4, is (1, 0, 0)) has inv = +-inf, and a * inv is then exactly the
+// IEEE a / +-0 (qdiv). Nothing else is carried (round 4: the sphere quadratic's d.d and its reciprocal,
+// and the `safe` flag, are recomputed where they are used — five registers fewer in every walk's live
+// state: C2's 4-wave kernel 124 -> 108 B/lane of scratch, C4's 192 -> 176).
 struct RayX {
   V3 o, d;
   double tm;
   V3 inv;      // RN(1 / d)
-  double a;    // dot d d (the sphere quadratic's `a`, Lib.hs:1092)
-  double inva; // RN(1 / a)
-  bool safe;
 };
 __device__ __forceinline__ bool div_ok(double b) { return in_range(b); }
 __device__ __forceinline__ RayX prep(const Ray& r) {
@@ -83,13 +81,15 @@ __device__ __forceinline__ RayX prep(const Ray& r) {
   x.d = r.d;
   x.tm = r.tm;
   x.inv = V3{1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z};
-  x.a = r.d.x * r.d.x + r.d.y * r.d.y + r.d.z * r.d.z;
-  x.inva = 1.0 / x.a;
-  x.safe = ((r.d.x == 0.0) | div_ok(r.d.x)) & ((r.d.y == 0.0) | div_ok(r.d.y)) & ((r.d.z == 0.0) | div_ok(r.d.z)) &
-           (fabs(r.o.x) <= 0x1p900) & (fabs(r.o.y) <= 0x1p900) & (fabs(r.o.z) <= 0x1p900);
   return x;
 }
 __device__ __forceinline__ Ray plain(const RayX& x) { return Ray{x.o, x.d, x.tm}; }
+// The division-free box test's condition (box_hit): a finite origin (|o| <= 2^900) and every direction
+// component either zero or in [2^-900, 2^900].
+__device__ __forceinline__ bool ray_safe(const RayX& r) {
+  return ((r.d.x == 0.0) | div_ok(r.d.x)) & ((r.d.y == 0.0) | div_ok(r.d.y)) & ((r.d.z == 0.0) | div_ok(r.d.z)) &
+         (fabs(r.o.x) <= 0x1p900) & (fabs(r.o.y) <= 0x1p900) & (fabs(r.o.z) <= 0x1p900);
+}
 // a / d exactly, given y = RN(1/d): a zero divisor gives a * y (= the IEEE a / +-0: +-inf with the
 // sign of a xor d, NaN for a = 0 or NaN), operands and quotient in [2^-900, 2^900] the Markstein
 // quotient (div_exact), anything else the IEEE division (a rare, divergent branch).
