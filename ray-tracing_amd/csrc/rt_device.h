@@ -68,7 +68,7 @@ __device__ __forceinline__ double div_exact(double a, double b, double y) {
 // of the Lambertian quirk, DESIGN.md §4.4, is (1, 0, 0)) has inv = +-inf, and a * inv is then exactly the
 // IEEE a / +-0 (qdiv). Nothing else is carried (round 4: the sphere quadratic's d.d and its reciprocal,
 // and the `safe` flag, are recomputed where they are used — five registers fewer in every walk's live
-// state: C2's 4-wave kernel 124 -> 108 B/lane of scratch, C4's 192 -> 176).
+// state: C2's 4-wave kernel 124 -> 108 B/lane of scratch, C4's 192 -> 176; DESIGN.md §3.2a).
 struct RayX {
   V3 o, d;
   double tm;

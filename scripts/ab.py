@@ -35,12 +35,15 @@ def build(a):
     shutil.rmtree(src, ignore_errors=True)
     if a.rev:
         wt = "/tmp/ab_worktree"
+        # (the revision is resolved in the main repository: "HEAD" inside the worktree is the worktree's)
+        sha = subprocess.run(["git", "-C", ROOT, "rev-parse", a.rev], check=True, capture_output=True,
+                             text=True).stdout.strip()
         if not os.path.isdir(wt):
-            subprocess.run(["git", "-C", ROOT, "worktree", "add", "-f", "--detach", wt, a.rev], check=True)
-        subprocess.run(["git", "-C", wt, "checkout", "-q", "--detach", a.rev], check=True)
+            subprocess.run(["git", "-C", ROOT, "worktree", "add", "-f", "--detach", wt, sha], check=True)
+        subprocess.run(["git", "-C", wt, "checkout", "-q", "--detach", sha], check=True)
         base = wt
     else:
-        base = ROOT
+        base, sha = ROOT, ""
     os.makedirs(src)
     for d in ("ray-tracing_amd", "include"):
         shutil.copytree(os.path.join(base, d), os.path.join(src, d), ignore=shutil.ignore_patterns("build", "__pycache__"))
@@ -62,7 +65,7 @@ def build(a):
     shutil.copytree(os.path.join(src, "ray-tracing_amd", "rtamd"), os.path.join(out, "ray-tracing_amd", "rtamd"))
     shutil.copy(os.path.join(src, "ray-tracing_amd", "build", "librtamd.so"), os.path.join(out, "ray-tracing_amd", "build"))
     shutil.copy(os.path.join(ROOT, "tests", "golden", "earthmap_rgb8.npz"), os.path.join(out, "tests", "golden"))
-    what = (f"rev {a.rev}" if a.rev else "working tree") + (f", patch {a.patch}" if a.patch else "") + (
+    what = (f"rev {a.rev} ({sha[:10]})" if a.rev else "working tree") + (f", patch {a.patch}" if a.patch else "") + (
         f", flags {a.flags}" if a.flags else "")
     print(f"_var_{a.name}: {what}")
 
