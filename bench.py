@@ -124,20 +124,23 @@ def _pmc_summary(args):
         return json.load(f), path
 
 
-def pmc_traffic(args, kernel_ms):
+def pmc_traffic(args, kernel_ms, dispatches=1):
     """HBM traffic of the render kernel from the committed rocprofv3 PMC summary of the same
-    config (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE, bytes per launch), as GB/s over
-    this run's live kernel time, and the bytes per launch. None when no summary matches the launched
-    kernel selection."""
+    config (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE, bytes per dispatch), as GB/s over
+    this run's live kernel time, and the bytes per frame step: a step of `dispatches` kernel launches
+    (chunk batches, rt_launch_info.chunk_batches: C5 13) moves that many times the summary's
+    per-dispatch bytes in its kernel time. None when no summary matches the launched kernel selection."""
     s, path = _pmc_summary(args)
     if s is None:
         return None, None, "no PMC summary for this kernel selection"
     b = s.get("derived", {}).get("hbm_bytes")
     if b is None:
         return None, None, f"{os.path.basename(path)} has no FETCH_SIZE/WRITE_SIZE"
-    return round(b / (kernel_ms * 1e-3) / 1e9, 3), round(b), (
-        f"{os.path.relpath(path, ROOT)}: {b / 1e6:.1f} MB/launch HBM (FETCH_SIZE x2 + WRITE_SIZE) over the "
-        f"live kernel time; profiled launch {s['avg_duration_s'] * 1e3:.1f} ms")
+    step = b * dispatches
+    return round(step / (kernel_ms * 1e-3) / 1e9, 3), round(step), (
+        f"{os.path.relpath(path, ROOT)}: {b / 1e6:.1f} MB per kernel dispatch HBM (FETCH_SIZE x2 + WRITE_SIZE) "
+        f"x {dispatches} dispatch(es) per step, over the live kernel time; profiled dispatch "
+        f"{s['avg_duration_s'] * 1e3:.1f} ms")
 
 
 def pmc_valu(args):
@@ -460,12 +463,14 @@ def main():
             fl32 = f32 * samples_per_launch / secs / 1e12
             # fp64-equivalent rate: an fp32 op costs half an fp64 one at the vector peaks (157.3 vs 78.6 TF)
             eq = fl + fl32 * FP64_PEAK_TFLOPS / FP32_PEAK_TFLOPS
-            traffic, tbytes, tnote = pmc_traffic(args, kernel_avg)
+            dispatches = max(1, int(ctx.last_launch().get("chunk_batches", 1)))
+            traffic, tbytes, tnote = pmc_traffic(args, kernel_avg, dispatches)
             off = algorithmic_offchip_bytes(cfg, p, scene)
             out["roofline"] = {
                 "bound": "fp64-valu", "achieved": round(eq, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(eq / FP64_PEAK_TFLOPS, 5),
                 "traffic": traffic, "traffic_unit": "GB/s", "traffic_bytes_per_launch": tbytes,
+                "kernel_dispatches_per_step": dispatches,
                 "algorithmic_offchip_bytes": off,
                 "traffic_over_algorithmic": round(tbytes / off["total"], 3) if tbytes else None,
                 "traffic_note": tnote,

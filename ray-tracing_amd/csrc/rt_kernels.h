@@ -66,6 +66,8 @@ struct RenderArgs {
   int leaf_stop;             // 4-wide walk: leaf step once <= leaf_stop/64 of live lanes seek a leaf
   int box_first;             // binary walk: box-only steps while > box_first/64 of live lanes are at BVH
                              // nodes (64: never)
+  int med_batch;             // binary walk of media worlds: lanes at a medium wait until this many are there
+                             // (or nothing else walks); 0: never wait
   uint32_t rev_tiles;        // RTAMD_TILE_REV: the slab's tiles run last to first (this count; 0: in order)
   uint8_t* out_rgb;  // tier B: slab; tier A: image
   double* out_lin;
@@ -513,7 +515,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     const int live = __popcll(__ballot(true));
     const int stop = (live * A.trav_stop) >> 6;
     const int ls = (F & F_WIDE) ? A.leaf_stop : A.box_first;
-    walk_until<F>(S, t, walking, kEps, stk, stride, joint, stop, (live * ls) >> 6, cnt, g, side);
+    walk_until<F>(S, t, walking, kEps, stk, stride, joint, stop, (live * ls) >> 6, cnt, g, side, A.med_batch);
     ready = !walking;
     if constexpr ((F & F_COUNT) != 0) {
       const unsigned long long s2 = stamp();

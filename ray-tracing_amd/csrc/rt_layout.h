@@ -25,6 +25,12 @@
                                and on the roots), so that a walk schedules box steps without a load */
 #define RT_WROOT 0x20000000 /* rt_node.c flag of an RT_BVH_ORDERED node whose subtree has a 4-wide tree, */
 #define RT_WROOT_MASK 0x3ffffff /* whose root index is (c >> 2) & RT_WROOT_MASK (mixed walks) */
+#define RT_ISMED 0x04000000 /* node-id tag: a ConstantMedium (set like RT_ISBOX), so that a walk can hold the
+                               lanes at media back without a load (node ids stay below 2^26) */
+#define RT_IDTAGS (RT_ISBOX | RT_ISMED) /* the kind tags every walk masks off a node id */
+#define RT_SAMEBOX RT_IDTAGS /* both tags (a BVH node is no medium): the left child of a reference-order BVH node
+                                whose box is bit-identical to its parent's, entered right after the parent's
+                                passing test under the same bound: its own test would pass too */
 #define RT_SUB 0x20000000   /* node-id tag (walks in the reference's order): inside a re-bounded,
                                media-free subtree (below an RT_BVH_ORDERED node) */
 #define RT_CHAIN_PRIM 0x100 /* device node type flag: Translate/Rotate chain ending in a primitive */

@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <functional>
 #include <string>
+#include <cstring>
 #include <vector>
 
 using namespace rtd;
@@ -286,8 +287,8 @@ int prepare_scene(const rt_scene_desc* din, uint32_t flags, PreparedScene& P) {
     // frames) are re-bounded; RTAMD_SKELETON=0 keeps the caller's tree as is.
     dd.world_root = rebuild_for_device(nodes, din->world_root);
   }
-  if ((int)nodes.size() >= RT_ISBOX)
-    return fail_with(RT_E_INVALID, "rt_upload_scene: too many nodes (ids must stay below 2^27)");
+  if ((int)nodes.size() >= RT_ISMED)
+    return fail_with(RT_E_INVALID, "rt_upload_scene: too many nodes (ids must stay below 2^26)");
   dd.nodes = nodes.data();
   dd.n_nodes = (int)nodes.size();
   const rt_scene_desc* d = &dd;
@@ -325,18 +326,27 @@ int prepare_scene(const rt_scene_desc* din, uint32_t flags, PreparedScene& P) {
   if (d->image_pool_bytes < 0 || (d->image_pool_bytes > 0 && !d->image_pool))
     return fail_with(RT_E_INVALID, "rt_upload_scene: image_pool is null but image_pool_bytes > 0");
   P.rebuilt_bvh = dd.world_root != din->world_root;
-  // BVH children that are BVH nodes carry RT_ISBOX in the device copy (every walk masks it off), so
-  // that the walks' box-first scheduling knows a node's kind without loading it
+  // BVH children that are BVH nodes carry RT_ISBOX in the device copy, media RT_ISMED (every walk masks
+  // them off), so that the walks' step scheduling knows a node's kind without loading it
   const std::vector<rt_node> untagged = v.nodes;  // (the mixed walk's wide trees are built from it)
-  auto is_bvh = [&](int id) { return (untagged[id].type & RT_TYPE_MASK) == RT_NODE_BVH; };
+  auto is_bvh_id = [](const std::vector<rt_node>& ns, int id) { return (ns[id].type & RT_TYPE_MASK) == RT_NODE_BVH; };
+  auto kind_tag = [&](int id) {
+    const int ty = untagged[id].type & RT_TYPE_MASK;
+    return ty == RT_NODE_BVH ? RT_ISBOX : (ty == RT_NODE_CONSTANT_MEDIUM ? RT_ISMED : 0);
+  };
   for (rt_node& x : v.nodes)
     if ((x.type & RT_TYPE_MASK) == RT_NODE_BVH) {
-      if (is_bvh(x.a)) x.a |= RT_ISBOX;
-      if (is_bvh(x.b)) x.b |= RT_ISBOX;
+      // a reference-order node always enters its left child next, under the bound its own test had: a
+      // left child with the same box (makeBVH over a span dominated by one huge object, e.g. the fog
+      // sphere of next_week_final) passes whenever the parent passed (RT_SAMEBOX)
+      const bool same = !(x.c & RT_BVH_ORDERED) && is_bvh_id(untagged, x.a) &&
+                        std::memcmp(untagged[x.a].f, x.f, 6 * sizeof(double)) == 0;
+      x.a |= same ? RT_SAMEBOX : kind_tag(x.a);
+      x.b |= kind_tag(x.b);
     }
   P.nodes = std::move(v.nodes);
-  P.world = d->world_root | (is_bvh(d->world_root) ? RT_ISBOX : 0);
-  P.world_ref = din->world_root | (is_bvh(din->world_root) ? RT_ISBOX : 0);
+  P.world = d->world_root | kind_tag(d->world_root);
+  P.world_ref = din->world_root | kind_tag(din->world_root);
   P.world_root = d->world_root;
   P.lights = d->lights_root;
   P.features = scene_features(d);

@@ -338,6 +338,8 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   // 48 416, 32 406, 16 398, 8 413; C3's Cornell kernel does not take it)
   const char* box_env = std::getenv("RTAMD_BOX_FIRST");
   A.box_first = box_env ? std::max(0, std::min(64, std::atoi(box_env))) : 16;
+  const char* med_env = std::getenv("RTAMD_MED_BATCH");
+  A.med_batch = med_env ? std::max(0, std::min(64, std::atoi(med_env))) : 0;
   // work order only (the chunk sums do not depend on it): the slab's tiles last to first
   A.rev_tiles = env_off("RTAMD_TILE_REV") || !std::getenv("RTAMD_TILE_REV") ? 0u : (uint32_t)per_shard;
   const unsigned var = variant_for(c->features);

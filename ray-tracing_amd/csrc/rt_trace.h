@@ -1,5 +1,17 @@
 // rt_trace.h — intersection, traversal, light sampling, textures and scattering (device).
 #pragma once
+#ifndef RTX_NO_MEDB
+#define RTX_NO_MEDB 0
+#endif
+#ifndef RTX_FUSE
+#define RTX_FUSE 8
+#endif
+#ifndef RTX_NO_SAME
+#define RTX_NO_SAME 0
+#endif
+#ifndef RTX_NO_ALT
+#define RTX_NO_ALT 0
+#endif
 #include "rt_device.h"
 
 namespace rtd {
@@ -193,7 +205,12 @@ __device__ __forceinline__ bool rect_hit(int plane, double i0, double i1, double
 }
 
 // hit Sphere's t (Lib.hs:1081-1095): strict tmin < t < tmax, quotients exact.
-__device__ __forceinline__ bool sphere_t(V3 sc, double sr, const RayX& r, double t_min, double t_max, double& tout) {
+// hit Sphere's t (Lib.hs:1081-1095): strict tmin < t < tmax, quotients exact. `two` (a ConstantMedium's
+// boundary, Lib.hs:1054-1059): also its second query over (t1 + eps, inf), from the same two roots (the
+// same ray and sphere give the same roots; temp1 itself never exceeds temp1 + eps, so the second query
+// is temp2 when the first took temp1, else nothing): t1 = the first query's t, tout = the second's.
+__device__ __forceinline__ bool sphere_t(V3 sc, double sr, const RayX& r, double t_min, double t_max, double& tout,
+                                         bool two, double& t1) {
   const V3 oc = r.o - sc;
   const double a = r.d.x * r.d.x + r.d.y * r.d.y + r.d.z * r.d.z;  // (Lib.hs:1092)
   const double inva = 1.0 / a;
@@ -208,10 +225,27 @@ __device__ __forceinline__ bool sphere_t(V3 sc, double sr, const RayX& r, double
     temp1 = n1 / a;
     temp2 = n2 / a;
   }
-  if (t_min < temp1 && temp1 < t_max) tout = temp1;
-  else if (t_min < temp2 && temp2 < t_max) tout = temp2;
-  else return false;
+  if (t_min < temp1 && temp1 < t_max) {
+    tout = temp1;
+    if (two) {
+      t1 = temp1;
+      tout = temp2;
+      return temp1 + kEps < temp2 && temp2 < INFINITY;
+    }
+  } else if (t_min < temp2 && temp2 < t_max) {
+    tout = temp2;
+    if (two) {
+      t1 = temp2;
+      return false;
+    }
+  } else {
+    return false;
+  }
   return true;
+}
+__device__ __forceinline__ bool sphere_t(V3 sc, double sr, const RayX& r, double t_min, double t_max, double& tout) {
+  double t1;
+  return sphere_t(sc, sr, r, t_min, t_max, tout, false, t1);
 }
 // log for hit ConstantMedium's distance draw (Lib.hs:1074). Not inlined, like sphere_uv: the draw happens
 // inside the walk, and OCML's fp64 log coefficients held across the render loop cost the full variant
@@ -272,15 +306,17 @@ __device__ __forceinline__ void cuboid_face(const rt_node* n, int i, int& plane,
 // faces, each with the full [tmin, tmax]: the later face keeps a tie.
 template <unsigned F>
 __device__ __forceinline__ bool prim_t(const Scene& S, const rt_node* n, const RayX& r, double t_min, double t_max,
-                                       double& t, int& sub) {
+                                       double& t, int& sub, bool& two, double& t1) {
   const int type = n->type & RT_TYPE_MASK;
   sub = 0;
-  if (!(F & (F_RECT | F_MOVING)) || type == RT_NODE_SPHERE) return sphere_t(vload(n->f), n->f[3], r, t_min, t_max, t);
+  // (`two`: a medium's boundary asks for both of its queries; they stay two calls but for spheres)
+  two = two && (type == RT_NODE_SPHERE || ((F & F_MOVING) && type == RT_NODE_MOVING_SPHERE));
+  if (!(F & (F_RECT | F_MOVING)) || type == RT_NODE_SPHERE) return sphere_t(vload(n->f), n->f[3], r, t_min, t_max, t, two, t1);
   if ((F & F_MOVING) && type == RT_NODE_MOVING_SPHERE) {  // Lib.hs:1106-1108
     const rt_node* e = n + 1;
     const V3 c0 = vload(n->f), c1 = vload(n->f + 3);
     const V3 sc = c0 + scale((r.tm - e->f[0]) / e->f[2], c1 - c0);
-    return sphere_t(sc, e->f[3], r, t_min, t_max, t);
+    return sphere_t(sc, e->f[3], r, t_min, t_max, t, two, t1);
   }
   if constexpr (!(F & F_RECT)) return false;
   if (type == RT_NODE_CUBOID) {
@@ -300,6 +336,13 @@ __device__ __forceinline__ bool prim_t(const Scene& S, const rt_node* n, const R
   if (type >= RT_NODE_RECT_XY && type <= RT_NODE_RECT_YZ)
     return rect_t(type - RT_NODE_RECT_XY, n->f[0], n->f[1], n->f[2], n->f[3], n->f[4], r, t_min, t_max, t);
   return false;
+}
+template <unsigned F>
+__device__ __forceinline__ bool prim_t(const Scene& S, const rt_node* n, const RayX& r, double t_min, double t_max,
+                                       double& t, int& sub) {
+  bool two = false;
+  double t1;
+  return prim_t<F>(S, n, r, t_min, t_max, t, sub, two, t1);
 }
 template <unsigned F>
 __device__ __forceinline__ void prim_record(const Scene& S, const rt_node* n, int sub, const Ray& r, double t, Hit& h) {
@@ -454,7 +497,7 @@ __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr
   int sp = 0;
   int node = root;
   for (;;) {
-    const rt_node* n = &S.nodes[node & ~RT_ISBOX];
+    const rt_node* n = &S.nodes[node & ~RT_IDTAGS];
     const int tf = n->type;
     const int type = tf & RT_TYPE_MASK;
     if (type == RT_NODE_BVH) {
@@ -848,8 +891,9 @@ __device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, const rt_node
   bool ok;
 #pragma nounroll
   for (int q = 0;; ++q) {
-    ok = prim_t<F>(S, p, rx, lo, hi, tt, sub);
-    if (!(medium && ok && q == 0)) break;
+    bool two = !RTX_NO_ALT && medium && q == 0;  // (a sphere boundary answers both queries at once)
+    ok = prim_t<F>(S, p, rx, lo, hi, tt, sub, two, t1);
+    if (two || !(medium && ok && q == 0)) break;
     t1 = tt;  // hit ConstantMedium's first boundary query; the second starts just past it
     lo = t1 + kEps;
   }
@@ -1011,7 +1055,7 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
     leaf_slot = t.node < 0;
   }
   // (mixed walks: the RT_SUB tag of the node id says whether it lies below an RT_BVH_ORDERED node)
-  int id = leaf_slot ? (~t.node | kSlotTag) : (t.node & ~(RT_SUB | RT_ISBOX));
+  int id = leaf_slot ? (~t.node | kSlotTag) : (t.node & ~(RT_SUB | RT_IDTAGS));
   int tag = leaf_slot ? RT_SUB : (kRefMixed<F> ? (t.node & RT_SUB) : 0);
   bool refsem = t.ref && !tag;
   const rt_node* n = leaf_slot ? &S.leaves[~t.node] : &S.nodes[id];
@@ -1023,16 +1067,18 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
    // the same bound in the same order, only in fewer walk steps (C4's skeleton: the fog's three
    // ancestors; C4 at 100 spp 253 -> 248 ms, C3 322 -> 318 ms). Not in the 4-wide kernels, whose binary
    // steps are tie redos only (+16 B/lane of scratch there).
-   constexpr int kFuse = (F & F_WIDE) ? 0 : 8;
+   constexpr int kFuse = (F & F_WIDE) ? 0 : RTX_FUSE;
    for (int fuse = 0;; ++fuse) {
     if (fuse) {
-      id = t.node & ~(RT_SUB | RT_ISBOX);
+      id = t.node & ~(RT_SUB | RT_IDTAGS);
       tag = kRefMixed<F> ? (t.node & RT_SUB) : 0;
       refsem = t.ref && !tag;
       n = &S.nodes[id];
     }
-    if constexpr ((F & F_COUNT) != 0) ++cnt.box;
-    if (box_hit(n->f, t.ray, t_min, refsem ? t.closest : closest_up<F>(t), joint)) {
+    // (RT_SAMEBOX: the parent's box, just passed under this bound)
+    const bool same = !RTX_NO_SAME && (t.node & RT_IDTAGS) == RT_SAMEBOX;
+    if constexpr ((F & F_COUNT) != 0) cnt.box += !same;
+    if (same || box_hit(n->f, t.ray, t_min, refsem ? t.closest : closest_up<F>(t), joint)) {
       const int c = n->c;
       const bool ord = (c & RT_BVH_ORDERED) && !t.redo;
       if constexpr ((F & F_MIXW) != 0) {
@@ -1118,7 +1164,8 @@ __device__ __forceinline__ void wide_leaf(const Scene& S, Trav& t, double t_min,
 // most `leaf_stop` walking lanes still look for their first leaf, then one leaf step.
 template <unsigned F, class R>
 __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walking, double t_min, int* stk, int stride,
-                                           bool joint, int stop, int leaf_stop, Cnt& cnt, R& g, Side& side) {
+                                           bool joint, int stop, int leaf_stop, Cnt& cnt, R& g, Side& side,
+                                           int med_batch = 0) {
   if constexpr ((F & F_WIDE) == 0) {
     for (;;) {
       const int n_walk = __popcll(__ballot(walking));
@@ -1136,13 +1183,21 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
         if (walking) {
           if ((F & F_MIXW) && t.node < 0) ty = S.leaves[~t.node].type & RT_TYPE_MASK;
           else if (box_id) ty = RT_NODE_BVH;
-          else ty = S.nodes[t.node & ~(RT_SUB | RT_ISBOX)].type & RT_TYPE_MASK;
+          else ty = S.nodes[t.node & ~(RT_SUB | RT_IDTAGS)].type & RT_TYPE_MASK;
         }
       }
       bool go = walking;
       if constexpr (kBoxFirst) {
         const int n_box = __popcll(__ballot(at_box));
-        if (leaf_stop < n_walk && n_box > leaf_stop) go = walking && at_box;
+        if (leaf_stop < n_walk && n_box > leaf_stop) {
+          go = walking && at_box;
+        } else if ((F & F_MEDIA) && med_batch > 0 && !RTX_NO_MEDB) {
+          // lanes at a medium (two boundary queries, a draw, a log) wait until med_batch of them are there
+          // or nothing else walks, so that fewer steps carry the medium code
+          const bool at_med = walking && t.node >= 0 && (t.node & (RT_WNODE | RT_IDTAGS)) == RT_ISMED;
+          const int n_med = __popcll(__ballot(at_med));
+          if (n_med < med_batch && n_med < n_walk) go = walking && !at_med;
+        }
       }
       if constexpr ((F & F_COUNT) != 0) {  // counting build: wave steps, and the node kinds each one runs
         ++cnt.islot;                        // (every lane counts a step: / 64 per wave)
@@ -1159,7 +1214,7 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
         const bool inst = ty == RT_NODE_TRANSLATE || ty == RT_NODE_ROTATE;
         bool frame = false;
         if (inst) {
-          const int nid = t.node < 0 ? -1 : (t.node & ~(RT_SUB | RT_ISBOX));
+          const int nid = t.node < 0 ? -1 : (t.node & ~(RT_SUB | RT_IDTAGS));
           const int tf = t.node < 0 ? S.leaves[~t.node].type : S.nodes[nid].type;
           frame = !(tf & RT_CHAIN_PRIM);
         }
@@ -1276,7 +1331,7 @@ __device__ __forceinline__ bool trav_finish(const Scene& S, const Trav& t, const
 // the same value: pdf(BVH) = box ? wl*(pdf(l)+0) + wr*(pdf(r)+0) : 0. Depth <= RT_LIGHT_DEPTH.
 template <unsigned F, int D>
 __device__ __forceinline__ double htbl_pdf_value(const Scene& S, int id, V3 origin, V3 v, const RayX& r) {
-  id &= ~RT_ISBOX;
+  id &= ~RT_IDTAGS;
   const rt_node* n = &S.nodes[id];
   const int type = n->type & RT_TYPE_MASK;
   Hit hh;
@@ -1299,9 +1354,9 @@ __device__ __forceinline__ double htbl_pdf_value(const Scene& S, int id, V3 orig
     if (type == RT_NODE_BVH) {
       if (!box_hit(n->f, r, kEps, INFINITY, false)) return 0.0;
       const double left_pdf = htbl_pdf_value<F, D - 1>(S, n->a, origin, v, r) + 0;
-      const double left_w = (double)S.nodes[n->a & ~RT_ISBOX].c / (double)n->c;
+      const double left_w = (double)S.nodes[n->a & ~RT_IDTAGS].c / (double)n->c;
       const double right_pdf = htbl_pdf_value<F, D - 1>(S, n->b, origin, v, r) + 0;
-      const double right_w = (double)S.nodes[n->b & ~RT_ISBOX].c / (double)n->c;
+      const double right_w = (double)S.nodes[n->b & ~RT_IDTAGS].c / (double)n->c;
       return left_w * left_pdf + right_w * right_pdf;
     }
   }
@@ -1311,11 +1366,11 @@ __device__ __forceinline__ double htbl_pdf_value(const Scene& S, int id, V3 orig
 // htblRandom (Lib.hs:707-724)
 template <class R>
 __device__ inline V3 htbl_random(const Scene& S, int id, V3 o, R& g) {
-  if (id >= 0) id &= ~RT_ISBOX;
+  if (id >= 0) id &= ~RT_IDTAGS;
   while (id >= 0 && (S.nodes[id].type & RT_TYPE_MASK) == RT_NODE_BVH) {
     const rt_node* n = &S.nodes[id];
     const double rd = g.draw();
-    id = (rd < (double)S.nodes[n->a & ~RT_ISBOX].c / (double)n->c ? n->a : n->b) & ~RT_ISBOX;
+    id = (rd < (double)S.nodes[n->a & ~RT_IDTAGS].c / (double)n->c ? n->a : n->b) & ~RT_IDTAGS;
   }
   if (id < 0) return v3(1, 0, 0);
   const rt_node* n = &S.nodes[id];
