@@ -127,6 +127,7 @@ struct Scene {
   int lights;
   int ref_walk;   // media or instance frames: the replacement loop walks the caller's tree in the
                   // reference's own order (media draw order, Lib.hs:971-988,1053-1080)
+  int frames;     // deepest nesting of instance frames in the world trees (the lanes' Side slots)
   double bg[3];
 };
 

@@ -66,12 +66,12 @@ struct RenderArgs {
   int leaf_stop;             // 4-wide walk: leaf step once <= leaf_stop/64 of live lanes seek a leaf
   int box_first;             // binary walk: box-only steps while > box_first/64 of live lanes are at BVH
                              // nodes (64: never)
-  int med_batch;             // binary walk of media worlds: lanes at a medium wait until this many are there
-                             // (or nothing else walks); 0: never wait
   uint32_t rev_tiles;        // RTAMD_TILE_REV: the slab's tiles run last to first (this count; 0: in order)
   uint8_t* out_rgb;  // tier B: slab; tier A: image
   double* out_lin;
   uint64_t* gens;  // tier A: per-column (seed, gamma), updated in place
+  int med_batch;   // binary walk of media worlds: lanes at a medium wait until this many are there (or
+                   // nothing else walks); 0: never wait
 };
 
 // Slab pixel index -> image pixel (tile-major, 8x8 blocks inside a tile). Slab indices are < 2^32
@@ -365,7 +365,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
   RngPhilox g;
   g.init(A.seed, 0, 0);
   Trav t;  // the segment's ray lives only here between segments (no second copy is carried)
-  Side side{side_p, stride};
+  Side side{side_p, stride, S.frames};
   Cnt cnt{};
   if constexpr ((F & F_COUNT) != 0) cnt.prof = A.prof;
   unsigned long long segs = 0, blocks = 0, samples = 0, ph_setup = 0, ph_trav = 0, ph_shade = 0;

@@ -354,6 +354,7 @@ int prepare_scene(const rt_scene_desc* din, uint32_t flags, PreparedScene& P) {
   P.stack_need = std::max(v.stack_need[d->world_root], v.stack_need[din->world_root]);
   // The replacement loop takes every world whose frames nest at most RT_MAX_FRAMES deep (its Side
   // slots); worlds with media or frames walk the caller's tree in the reference's order.
+  P.frame_depth = std::max(v.frame_depth[d->world_root], v.frame_depth[din->world_root]);
   const bool frames = v.frame_depth[d->world_root] > 0;
   P.replace_ok = v.frame_depth[d->world_root] <= RT_MAX_FRAMES;
   P.ref_walk = (P.features & F_MEDIA) || frames;

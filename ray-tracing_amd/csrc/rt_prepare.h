@@ -21,6 +21,7 @@ struct PreparedScene {
   int lights = -1;
   unsigned features = 0;          // rtd::F_* bits of the scene (+ F_FRAMES)
   int stack_need = 0;             // binary / mixed walk stack bound (entries)
+  int frame_depth = 0;            // deepest nesting of instance frames (the device tree's or the caller's)
   int wide_stack_need = 0;        // 4-wide walk stack bound
   bool rebuilt_bvh = false, mixed_wide = false, replace_ok = false, ref_walk = false;
 };

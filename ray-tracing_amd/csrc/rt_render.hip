@@ -339,7 +339,9 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   const char* box_env = std::getenv("RTAMD_BOX_FIRST");
   A.box_first = box_env ? std::max(0, std::min(64, std::atoi(box_env))) : 16;
   const char* med_env = std::getenv("RTAMD_MED_BATCH");
-  A.med_batch = med_env ? std::max(0, std::min(64, std::atoi(med_env))) : 0;
+  // lanes at a medium wait for 4 of them (C4 at 100 spp, same box: 0 249.0 ms, 4 245.3, 8 245.9, 16 295 at
+  // the time's 10-wave occupancy)
+  A.med_batch = med_env ? std::max(0, std::min(64, std::atoi(med_env))) : 4;
   // work order only (the chunk sums do not depend on it): the slab's tiles last to first
   A.rev_tiles = env_off("RTAMD_TILE_REV") || !std::getenv("RTAMD_TILE_REV") ? 0u : (uint32_t)per_shard;
   const unsigned var = variant_for(c->features);
@@ -362,7 +364,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   // variant on the replacement loop 3 (C4 at 100 spp: 90.9 vs 87.5 Msamples/s at 2), on the
   // per-sample loop 2 despite 784 B/lane of scratch (C4 35.2 vs 23.4 at 1 wave, 9.1 at 3)
   int waves = (var == kVarSpheres || loop) ? waves_target(3) : waves_target(is_full(var) ? 2 : 1);
-  const int side_ints = (var & F_FRAMES) && loop == 1 ? kSideInts : 0;  // Side slots after the stacks
+  const int side_ints = (var & F_FRAMES) && loop == 1 ? side_ints_for(c->scene.frames) : 0;  // Side slots after the stacks
   // LDS-staged kernel when the traversal's node array plus the stacks fit one CU's 160 KiB
   // (RTAMD_LDS=0 disables it for A/B runs).
   if (!count && !env_off("RTAMD_LDS") && (!is_full(var) || loop)) {
@@ -503,6 +505,7 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
   S.world_ref = P.world_ref;
   S.lights = P.lights;
   S.ref_walk = P.ref_walk;
+  S.frames = std::max(1, std::min(RT_MAX_FRAMES, P.frame_depth));
   for (int i = 0; i < 3; ++i) S.bg[i] = din->background[i];
   c->features = P.features;
   c->n_nodes = (int)P.nodes.size();

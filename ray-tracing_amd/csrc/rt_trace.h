@@ -1,17 +1,5 @@
 // rt_trace.h — intersection, traversal, light sampling, textures and scattering (device).
 #pragma once
-#ifndef RTX_NO_MEDB
-#define RTX_NO_MEDB 0
-#endif
-#ifndef RTX_FUSE
-#define RTX_FUSE 8
-#endif
-#ifndef RTX_NO_SAME
-#define RTX_NO_SAME 0
-#endif
-#ifndef RTX_NO_ALT
-#define RTX_NO_ALT 0
-#endif
 #include "rt_device.h"
 
 namespace rtd {
@@ -205,12 +193,8 @@ __device__ __forceinline__ bool rect_hit(int plane, double i0, double i1, double
 }
 
 // hit Sphere's t (Lib.hs:1081-1095): strict tmin < t < tmax, quotients exact.
-// hit Sphere's t (Lib.hs:1081-1095): strict tmin < t < tmax, quotients exact. `two` (a ConstantMedium's
-// boundary, Lib.hs:1054-1059): also its second query over (t1 + eps, inf), from the same two roots (the
-// same ray and sphere give the same roots; temp1 itself never exceeds temp1 + eps, so the second query
-// is temp2 when the first took temp1, else nothing): t1 = the first query's t, tout = the second's.
-__device__ __forceinline__ bool sphere_t(V3 sc, double sr, const RayX& r, double t_min, double t_max, double& tout,
-                                         bool two, double& t1) {
+// hit Sphere's t (Lib.hs:1081-1095): strict tmin < t < tmax, quotients exact.
+__device__ __forceinline__ bool sphere_t(V3 sc, double sr, const RayX& r, double t_min, double t_max, double& tout) {
   const V3 oc = r.o - sc;
   const double a = r.d.x * r.d.x + r.d.y * r.d.y + r.d.z * r.d.z;  // (Lib.hs:1092)
   const double inva = 1.0 / a;
@@ -225,27 +209,10 @@ __device__ __forceinline__ bool sphere_t(V3 sc, double sr, const RayX& r, double
     temp1 = n1 / a;
     temp2 = n2 / a;
   }
-  if (t_min < temp1 && temp1 < t_max) {
-    tout = temp1;
-    if (two) {
-      t1 = temp1;
-      tout = temp2;
-      return temp1 + kEps < temp2 && temp2 < INFINITY;
-    }
-  } else if (t_min < temp2 && temp2 < t_max) {
-    tout = temp2;
-    if (two) {
-      t1 = temp2;
-      return false;
-    }
-  } else {
-    return false;
-  }
+  if (t_min < temp1 && temp1 < t_max) tout = temp1;
+  else if (t_min < temp2 && temp2 < t_max) tout = temp2;
+  else return false;
   return true;
-}
-__device__ __forceinline__ bool sphere_t(V3 sc, double sr, const RayX& r, double t_min, double t_max, double& tout) {
-  double t1;
-  return sphere_t(sc, sr, r, t_min, t_max, tout, false, t1);
 }
 // log for hit ConstantMedium's distance draw (Lib.hs:1074). Not inlined, like sphere_uv: the draw happens
 // inside the walk, and OCML's fp64 log coefficients held across the render loop cost the full variant
@@ -306,17 +273,15 @@ __device__ __forceinline__ void cuboid_face(const rt_node* n, int i, int& plane,
 // faces, each with the full [tmin, tmax]: the later face keeps a tie.
 template <unsigned F>
 __device__ __forceinline__ bool prim_t(const Scene& S, const rt_node* n, const RayX& r, double t_min, double t_max,
-                                       double& t, int& sub, bool& two, double& t1) {
+                                       double& t, int& sub) {
   const int type = n->type & RT_TYPE_MASK;
   sub = 0;
-  // (`two`: a medium's boundary asks for both of its queries; they stay two calls but for spheres)
-  two = two && (type == RT_NODE_SPHERE || ((F & F_MOVING) && type == RT_NODE_MOVING_SPHERE));
-  if (!(F & (F_RECT | F_MOVING)) || type == RT_NODE_SPHERE) return sphere_t(vload(n->f), n->f[3], r, t_min, t_max, t, two, t1);
+  if (!(F & (F_RECT | F_MOVING)) || type == RT_NODE_SPHERE) return sphere_t(vload(n->f), n->f[3], r, t_min, t_max, t);
   if ((F & F_MOVING) && type == RT_NODE_MOVING_SPHERE) {  // Lib.hs:1106-1108
     const rt_node* e = n + 1;
     const V3 c0 = vload(n->f), c1 = vload(n->f + 3);
     const V3 sc = c0 + scale((r.tm - e->f[0]) / e->f[2], c1 - c0);
-    return sphere_t(sc, e->f[3], r, t_min, t_max, t, two, t1);
+    return sphere_t(sc, e->f[3], r, t_min, t_max, t);
   }
   if constexpr (!(F & F_RECT)) return false;
   if (type == RT_NODE_CUBOID) {
@@ -336,13 +301,6 @@ __device__ __forceinline__ bool prim_t(const Scene& S, const rt_node* n, const R
   if (type >= RT_NODE_RECT_XY && type <= RT_NODE_RECT_YZ)
     return rect_t(type - RT_NODE_RECT_XY, n->f[0], n->f[1], n->f[2], n->f[3], n->f[4], r, t_min, t_max, t);
   return false;
-}
-template <unsigned F>
-__device__ __forceinline__ bool prim_t(const Scene& S, const rt_node* n, const RayX& r, double t_min, double t_max,
-                                       double& t, int& sub) {
-  bool two = false;
-  double t1;
-  return prim_t<F>(S, n, r, t_min, t_max, t, sub, two, t1);
 }
 template <unsigned F>
 __device__ __forceinline__ void prim_record(const Scene& S, const rt_node* n, int sub, const Ray& r, double t, Hit& h) {
@@ -587,10 +545,17 @@ __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr
 // Per-lane LDS slots of the resumable walk over worlds with instance frames (`stride` ints apart):
 // the world ray (restored when the last frame closes), the ids of the open frames, and of the
 // frames around the best hit (Trav::best_level of them).
-constexpr int kSideInts = 14 + 2 * RT_MAX_FRAMES;
+// Side ints per lane for frames nesting `frames` deep: the world ray (14), then the open frames and the
+// frames around the best hit. The host sizes the dynamic LDS per scene: C4's two-deep frames take 8 ints
+// per lane fewer than RT_MAX_FRAMES would. (The world ray's reciprocals stored as well, 6 more ints, would
+// spare prep's divisions when the last frame closes, but take C4's kernel past six blocks per CU: 243.8
+// -> 250.1 ms at 100 spp.)
+__host__ __device__ constexpr int side_ints_for(int frames) { return 14 + 2 * frames; }
+constexpr int kSideInts = side_ints_for(RT_MAX_FRAMES);
 struct Side {
   int* p;
   int stride;
+  int nf = RT_MAX_FRAMES;  // frame slots (the scene's deepest nesting)
   __device__ __forceinline__ void put_d(int i, double x) {
     const long long b = __double_as_longlong(x);
     p[(2 * i) * stride] = (int)(b & 0xffffffff);
@@ -607,8 +572,8 @@ struct Side {
     return Ray{v3(get_d(0), get_d(1), get_d(2)), v3(get_d(3), get_d(4), get_d(5)), get_d(6)};
   }
   __device__ __forceinline__ int& frame(int i) { return p[(14 + i) * stride]; }
-  __device__ __forceinline__ int& best(int i) { return p[(14 + RT_MAX_FRAMES + i) * stride]; }
-  __device__ __forceinline__ int best(int i) const { return p[(14 + RT_MAX_FRAMES + i) * stride]; }
+  __device__ __forceinline__ int& best(int i) { return p[(14 + nf + i) * stride]; }
+  __device__ __forceinline__ int best(int i) const { return p[(14 + nf + i) * stride]; }
 };
 // Trav::best_sub of a chain hit (kSubChain | the primitive's face) and of a ConstantMedium hit
 constexpr int kSubChain = 0x100, kSubMedium = -2;
@@ -891,9 +856,8 @@ __device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, const rt_node
   bool ok;
 #pragma nounroll
   for (int q = 0;; ++q) {
-    bool two = !RTX_NO_ALT && medium && q == 0;  // (a sphere boundary answers both queries at once)
-    ok = prim_t<F>(S, p, rx, lo, hi, tt, sub, two, t1);
-    if (two || !(medium && ok && q == 0)) break;
+    ok = prim_t<F>(S, p, rx, lo, hi, tt, sub);
+    if (!(medium && ok && q == 0)) break;
     t1 = tt;  // hit ConstantMedium's first boundary query; the second starts just past it
     lo = t1 + kEps;
   }
@@ -1000,13 +964,17 @@ template <unsigned F>
 __device__ __forceinline__ bool trav_pop_mixed(const Scene& S, Trav& t, const int* stk, int stride, Side& side,
                                                double t_min = kEps) {
   bool reb = false;
-  Ray pr;
   for (;;) {
     const bool end = t.sp == 0;
     const int e = end ? 0 : stk[(--t.sp) * stride];
     const bool frame = (F & F_FRAMES) && ((F & F_MIXW) ? (e >= 0 && (e & RT_FRAME)) : (e & RT_FRAME));
     if (end || !frame) {
       if ((F & F_FRAMES) && reb) {  // (also at the end: a tie redo walks on from it)
+        // the parent's ray, once for the run of closed frames: the world ray rebuilt through the frames
+        // still open. (Storing the world ray's reciprocals as well would save prep's divisions, but six
+        // more LDS ints per lane cost C4's kernel a block per CU: 12 -> 10 waves, 249 -> 288 ms.)
+        Ray pr = side.get_ray();
+        for (int k = 0; k < t.level; ++k) pr = enter_instance(&S.nodes[side.frame(k)], pr);
         t.ray = prep(pr);
         if constexpr ((F & F_MIXW) != 0) set_ray32(t, t_min);
       }
@@ -1015,8 +983,6 @@ __device__ __forceinline__ bool trav_pop_mixed(const Scene& S, Trav& t, const in
     }
     --t.level;  // a frame closes
     reb = true;
-    pr = side.get_ray();
-    for (int k = 0; k < t.level; ++k) pr = enter_instance(&S.nodes[side.frame(k)], pr);
   }
 }
 
@@ -1044,16 +1010,12 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
   // Mixed walks with wide subtrees (F_MIXW): a node is a flat id (| RT_SUB), a wide node
   // (RT_WNODE | index) or a leaf-table slot handed out by a wide node (~slot, negative); all of them
   // lie in re-bounded subtrees except flat ids without RT_SUB.
-  bool leaf_slot = false;
+  bool leaf_slot = false, to_wide = false;
   if constexpr ((F & F_MIXW) != 0) {
-    if (t.node >= 0 && (t.node & RT_WNODE)) {
-      if constexpr ((F & F_COUNT) != 0) ++cnt.wide;
-      refresh_ray32(t);
-      if (wide_node(S, t, stk, stride, t.node & ~RT_WNODE)) return true;
-      return trav_pop_mixed<F>(S, t, stk, stride, side);
-    }
+    to_wide = t.node >= 0 && (t.node & RT_WNODE);
     leaf_slot = t.node < 0;
   }
+  if (!to_wide) {
   // (mixed walks: the RT_SUB tag of the node id says whether it lies below an RT_BVH_ORDERED node)
   int id = leaf_slot ? (~t.node | kSlotTag) : (t.node & ~(RT_SUB | RT_IDTAGS));
   int tag = leaf_slot ? RT_SUB : (kRefMixed<F> ? (t.node & RT_SUB) : 0);
@@ -1067,7 +1029,7 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
    // the same bound in the same order, only in fewer walk steps (C4's skeleton: the fog's three
    // ancestors; C4 at 100 spp 253 -> 248 ms, C3 322 -> 318 ms). Not in the 4-wide kernels, whose binary
    // steps are tie redos only (+16 B/lane of scratch there).
-   constexpr int kFuse = (F & F_WIDE) ? 0 : RTX_FUSE;
+   constexpr int kFuse = (F & F_WIDE) ? 0 : 8;
    for (int fuse = 0;; ++fuse) {
     if (fuse) {
       id = t.node & ~(RT_SUB | RT_IDTAGS);
@@ -1076,15 +1038,16 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
       n = &S.nodes[id];
     }
     // (RT_SAMEBOX: the parent's box, just passed under this bound)
-    const bool same = !RTX_NO_SAME && (t.node & RT_IDTAGS) == RT_SAMEBOX;
+    const bool same = kRefMixed<F> && (t.node & RT_IDTAGS) == RT_SAMEBOX;
     if constexpr ((F & F_COUNT) != 0) cnt.box += !same;
     if (same || box_hit(n->f, t.ray, t_min, refsem ? t.closest : closest_up<F>(t), joint)) {
       const int c = n->c;
       const bool ord = (c & RT_BVH_ORDERED) && !t.redo;
       if constexpr ((F & F_MIXW) != 0) {
-        if (ord && (c & RT_WROOT)) {  // a re-bounded subtree with a 4-wide tree: walk that instead
-          t.node = RT_WNODE | ((c >> 2) & RT_WROOT_MASK);
-          return true;
+        if (ord && (c & RT_WROOT)) {  // a re-bounded subtree with a 4-wide tree: walk that instead, from its
+          t.node = RT_WNODE | ((c >> 2) & RT_WROOT_MASK);  // root node in this same step (below)
+          to_wide = true;
+          break;
         }
       }
       const bool flip = ord && comp(t.ray.d, c & 3) < 0;
@@ -1118,7 +1081,14 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
   } else {
     trav_leaf<F>(S, t, n, id, t_min, cnt, g, side, refsem);
   }
-  return trav_pop_mixed<F>(S, t, stk, stride, side, t_min);
+  if (!to_wide) return trav_pop_mixed<F>(S, t, stk, stride, side, t_min);
+  }
+  if constexpr ((F & F_MIXW) != 0) {  // a 4-wide node (RT_WNODE | index)
+    if constexpr ((F & F_COUNT) != 0) ++cnt.wide;
+    refresh_ray32(t);
+    if (wide_node(S, t, stk, stride, t.node & ~RT_WNODE)) return true;
+  }
+  return trav_pop_mixed<F>(S, t, stk, stride, side);
 }
 
 // ---- the 4-wide walk with postponed leaves (Aila & Laine's while-while, one postponed slot)
@@ -1191,7 +1161,7 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
         const int n_box = __popcll(__ballot(at_box));
         if (leaf_stop < n_walk && n_box > leaf_stop) {
           go = walking && at_box;
-        } else if ((F & F_MEDIA) && med_batch > 0 && !RTX_NO_MEDB) {
+        } else if ((F & F_MEDIA) && med_batch > 0) {
           // lanes at a medium (two boundary queries, a draw, a log) wait until med_batch of them are there
           // or nothing else walks, so that fewer steps carry the medium code
           const bool at_med = walking && t.node >= 0 && (t.node & (RT_WNODE | RT_IDTAGS)) == RT_ISMED;
