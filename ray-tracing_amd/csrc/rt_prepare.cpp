@@ -4,6 +4,9 @@
 // copies the result to the device, and `make -C tests/c asan` builds it (with rt_bvh.cpp,
 // rt_scene.cpp, rt_scenes.cpp) under AddressSanitizer + UBSan for the malformed-descriptor tests.
 #include "rt_prepare.h"
+#ifndef RT_FRAME_BATCH
+#define RT_FRAME_BATCH 0
+#endif
 
 #include <algorithm>
 #include <cstdint>
@@ -213,6 +216,13 @@ void mixed_wide_trees(PreparedScene& P, const std::vector<rt_node>& host, const 
         if ((flat[id].type & RT_TYPE_MASK) == RT_NODE_MOVING_SPHERE) leaves.push_back(flat[id + 1]);
       }
       w.child[k] = ~slot[id];
+#if RT_FRAME_BATCH
+      // an instance frame's slot loses bit 26 (every walk decodes ~(x | RT_ISMED)), so that walk_until
+      // tells lanes at frames without a load
+      const int fty = flat[id].type & RT_TYPE_MASK;
+      if ((fty == RT_NODE_TRANSLATE || fty == RT_NODE_ROTATE) && !(flat[id].type & RT_CHAIN_PRIM))
+        w.child[k] &= ~RT_ISMED;
+#endif
     }
   // Stack bound of the mixed walk: skeleton nodes left first, re-bounded binary nodes either child
   // first, a frame one entry, a wide node up to 3 stacked siblings (wide_node writes 3 slots) above the
@@ -223,7 +233,7 @@ void mixed_wide_trees(PreparedScene& P, const std::vector<rt_node>& host, const 
     int deepest = 0;
     for (int k = 0; k < RT_WIDE; ++k) {
       const int ch = wide[w].child[k];
-      deepest = std::max(deepest, ch >= 0 ? wneed(ch & ~RT_WNODE) : need_of(leaves[~ch].c));
+      deepest = std::max(deepest, ch >= 0 ? wneed(ch & ~RT_WNODE) : need_of(leaves[~(ch | RT_ISMED)].c));
     }
     return 3 + deepest;
   };

@@ -1,5 +1,8 @@
 // rt_trace.h — intersection, traversal, light sampling, textures and scattering (device).
 #pragma once
+#ifndef RT_FRAME_BATCH
+#define RT_FRAME_BATCH 0
+#endif
 #include "rt_device.h"
 
 namespace rtd {
@@ -1017,10 +1020,10 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
   }
   if (!to_wide) {
   // (mixed walks: the RT_SUB tag of the node id says whether it lies below an RT_BVH_ORDERED node)
-  int id = leaf_slot ? (~t.node | kSlotTag) : (t.node & ~(RT_SUB | RT_IDTAGS));
+  int id = leaf_slot ? (~(t.node | RT_ISMED) | kSlotTag) : (t.node & ~(RT_SUB | RT_IDTAGS));
   int tag = leaf_slot ? RT_SUB : (kRefMixed<F> ? (t.node & RT_SUB) : 0);
   bool refsem = t.ref && !tag;
-  const rt_node* n = leaf_slot ? &S.leaves[~t.node] : &S.nodes[id];
+  const rt_node* n = leaf_slot ? &S.leaves[~(t.node | RT_ISMED)] : &S.nodes[id];
   const int tf = n->type;
   const int type = tf & RT_TYPE_MASK;
   if (type == RT_NODE_BVH) {  // (never a leaf slot)
@@ -1151,7 +1154,7 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
       int ty = -1;
       if constexpr ((F & F_COUNT) != 0) {
         if (walking) {
-          if ((F & F_MIXW) && t.node < 0) ty = S.leaves[~t.node].type & RT_TYPE_MASK;
+          if ((F & F_MIXW) && t.node < 0) ty = S.leaves[~(t.node | RT_ISMED)].type & RT_TYPE_MASK;
           else if (box_id) ty = RT_NODE_BVH;
           else ty = S.nodes[t.node & ~(RT_SUB | RT_IDTAGS)].type & RT_TYPE_MASK;
         }
@@ -1166,7 +1169,16 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
           // or nothing else walks, so that fewer steps carry the medium code
           const bool at_med = walking && t.node >= 0 && (t.node & (RT_WNODE | RT_IDTAGS)) == RT_ISMED;
           const int n_med = __popcll(__ballot(at_med));
-          if (n_med < med_batch && n_med < n_walk) go = walking && !at_med;
+          if constexpr (RT_FRAME_BATCH && (F & F_MIXW) && (F & F_FRAMES)) {
+            // (likewise lanes at an instance frame found by a 4-wide node: its leaf slot lacks bit 26)
+            const bool at_frm = walking && t.node < 0 && !(t.node & RT_ISMED);
+            const int n_frm = __popcll(__ballot(at_frm));
+            const bool hold = (n_med < med_batch && at_med) || (n_frm < med_batch && at_frm);
+            go = walking && !hold;
+            if (__ballot(go) == 0) go = walking;  // (every walking lane held: all go)
+          } else {
+            if (n_med < med_batch && n_med < n_walk) go = walking && !at_med;
+          }
         }
       }
       if constexpr ((F & F_COUNT) != 0) {  // counting build: wave steps, and the node kinds each one runs
@@ -1185,7 +1197,7 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
         bool frame = false;
         if (inst) {
           const int nid = t.node < 0 ? -1 : (t.node & ~(RT_SUB | RT_IDTAGS));
-          const int tf = t.node < 0 ? S.leaves[~t.node].type : S.nodes[nid].type;
+          const int tf = t.node < 0 ? S.leaves[~(t.node | RT_ISMED)].type : S.nodes[nid].type;
           frame = !(tf & RT_CHAIN_PRIM);
         }
         kinds = (__ballot(go && ty == RT_NODE_BVH && !wide) ? K_BOX : 0u) | (__ballot(go && wide) ? K_WIDE : 0u) |
