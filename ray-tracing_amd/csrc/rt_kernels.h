@@ -3,6 +3,9 @@
 // variant's render kernels (so the variants compile in parallel), rt_render.hip the small kernels
 // and the host half of the C ABI. Kernel design: DESIGN.md §3.
 #pragma once
+#ifndef RT_LANE_LDS
+#define RT_LANE_LDS 1
+#endif
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -360,7 +363,17 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     wq[0] = 0u;
     wq[1] = 0u;
   }
-  int px = 0, row = 0, s = 0, s_end = 0, depth = 0;
+  // (the full variant's kernels keep the ints only acquisition and shading touch — pixel, row, the
+  // chunk's end sample, the path depth — in LDS next to the Side slots, out of the walk loop's VGPRs)
+  constexpr bool kLaneLds = kRefMixed<F> && RT_LANE_LDS;
+  int l_px = 0, l_row = 0, l_s_end = 0, l_depth = 0;
+  int* ex = side_p + side_ints_for(S.frames) * stride;
+  int& px = kLaneLds ? ex[0] : l_px;
+  int& row = kLaneLds ? ex[stride] : l_row;
+  int& s_end = kLaneLds ? ex[2 * stride] : l_s_end;
+  int& depth = kLaneLds ? ex[3 * stride] : l_depth;
+  px = 0, row = 0, s_end = 0, depth = 0;
+  int s = 0;
   V3 thr = v3(0, 0, 0), sum = v3(0, 0, 0);
   RngPhilox g;
   g.init(A.seed, 0, 0);
