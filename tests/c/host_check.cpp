@@ -10,7 +10,10 @@
 //   3. degenerate trees: a deep skewed spine (exponentially spaced centroids), a BVH over one item,
 //      nested instance frames beyond RT_MAX_FRAMES, a lights tree deeper than 2;
 //   4. the builder API with bad arguments;
-//   5. the oracle: small tier-A / tier-B renders, closest hits and function probes.
+//   5. the oracle: small tier-A / tier-B renders, closest hits and function probes;
+//   6. the device copy's node-id kind tags (rt::prepare_scene): RT_ISBOX on BVH children, RT_ISMED on
+//      media, RT_SAMEBOX only on the left child of a reference-order node with a bit-identical box,
+//      and mixed-walk leaf slots that decode into the leaf table.
 // Any sanitizer report aborts the process (-fno-sanitize-recover=all); exit 0 = clean.
 #include <cmath>
 #include <cstdint>
@@ -20,6 +23,7 @@
 #include <vector>
 
 #include "rt.h"
+#include "rt_prepare.h"
 
 extern "C" {
 int oracle_render(const rt_scene_desc* scene, const rt_camera* cam, const rt_render_params* p,
@@ -246,6 +250,46 @@ void oracle_runs(const rt_scene_desc& d, int cam_id, const char* what) {
   }
 }
 
+// 6. Kind tags of the device copy (the walks schedule steps by them without a load, RT_SAMEBOX skips a box
+// test): every tag must match the child it is on. Returns the number of RT_SAMEBOX tags.
+int device_tags(const rt_scene_desc& d, const char* what) {
+  rt::PreparedScene P;
+  CHECK(rt::prepare_scene(&d, 0, P) == RT_OK, "%s prepare: %s", what, rt_last_error());
+  const int n = (int)P.nodes.size();
+  auto type_of = [&](int id) { return P.nodes[id].type & RT_TYPE_MASK; };
+  int same = 0;
+  for (int i = 0; i < n; ++i) {
+    const rt_node& x = P.nodes[i];
+    if ((x.type & RT_TYPE_MASK) != RT_NODE_BVH) continue;
+    for (int side = 0; side < 2; ++side) {
+      const int c = side ? x.b : x.a, id = c & ~RT_IDTAGS, tag = c & RT_IDTAGS;
+      CHECK(id >= 0 && id < n, "%s node %d child id %d", what, i, id);
+      if (id < 0 || id >= n) continue;
+      const int ty = type_of(id);
+      if (tag == RT_SAMEBOX) {
+        ++same;
+        CHECK(side == 0 && ty == RT_NODE_BVH && !(x.c & RT_BVH_ORDERED) &&
+                  std::memcmp(P.nodes[id].f, x.f, 6 * sizeof(double)) == 0,
+              "%s node %d: RT_SAMEBOX on a child that is not its left, same-box BVH child", what, i);
+      } else {
+        const int want = ty == RT_NODE_BVH ? RT_ISBOX : (ty == RT_NODE_CONSTANT_MEDIUM ? RT_ISMED : 0);
+        CHECK(tag == want, "%s node %d child %d: tag %x, kind %d", what, i, id, tag, ty);
+      }
+    }
+  }
+  for (const rt_wnode& w : P.wnodes)
+    for (int k = 0; k < RT_WIDE; ++k) {
+      const int ch = w.child[k];
+      if (ch >= 0) {
+        CHECK((ch & ~RT_WNODE) < (int)P.wnodes.size(), "%s wide child %x", what, ch);
+      } else {
+        const int slot = ~(ch | RT_ISMED);
+        CHECK(slot >= 0 && slot < (int)P.leaves.size(), "%s leaf slot %d of %zu", what, slot, P.leaves.size());
+      }
+    }
+  return same;
+}
+
 }  // namespace
 
 int main() {
@@ -261,6 +305,10 @@ int main() {
       std::snprintf(what, sizeof what, "scene %d seed %lld", id, (long long)seed);
       CHECK(build_named(s, id, seed, earth), "%s build: %s", what, rt_last_error());
       trees(s.d, what);
+      const int same = device_tags(s.d, what);
+      // (next_week_final: the fog sphere's box is the root's and its two left descendants', in the device
+      // tree and again in the caller's tree that tie redos walk)
+      if (id == RT_SCENE_NEXT_WEEK_FINAL) CHECK(same >= 2, "%s: %d RT_SAMEBOX tags, expected at least 2", what, same);
       if (seed == 1024) {
         mutate(s.d, id == RT_SCENE_STRESS_SPHERES ? 100 : 400, what);
         oracle_runs(s.d, cams[id], what);
