@@ -363,11 +363,12 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     wq[0] = 0u;
     wq[1] = 0u;
   }
-  // (the full variant's kernels keep the ints only acquisition and shading touch — pixel, row, the
-  // chunk's end sample, the path depth — in LDS next to the Side slots, out of the walk loop's VGPRs)
-  constexpr bool kLaneLds = kRefMixed<F> && RT_LANE_LDS;
+  // (the ints only acquisition and shading touch — pixel, row, the chunk's end sample, the path depth —
+  // live in LDS after the stacks and Side slots, out of the walk loop's VGPRs; RT_LANE_LDS: 1 the
+  // reference-order kernels, 2 every replacement-loop kernel)
+  constexpr bool kLaneLds = RT_LANE_LDS >= 2 || (RT_LANE_LDS == 1 && kRefMixed<F>);
   int l_px = 0, l_row = 0, l_s_end = 0, l_depth = 0;
-  int* ex = side_p + side_ints_for(S.frames) * stride;
+  int* ex = side_p + ((F & F_FRAMES) ? side_ints_for(S.frames) : 0) * stride;
   int& px = kLaneLds ? ex[0] : l_px;
   int& row = kLaneLds ? ex[stride] : l_row;
   int& s_end = kLaneLds ? ex[2 * stride] : l_s_end;

@@ -364,8 +364,9 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   // variant on the replacement loop 3 (C4 at 100 spp: 90.9 vs 87.5 Msamples/s at 2), on the
   // per-sample loop 2 despite 784 B/lane of scratch (C4 35.2 vs 23.4 at 1 wave, 9.1 at 3)
   int waves = (var == kVarSpheres || loop) ? waves_target(3) : waves_target(is_full(var) ? 2 : 1);
-  // Side slots after the stacks, then (reference-order kernels) the 4 lane ints philox_loop2 keeps in LDS
-  const int side_ints = (var & F_FRAMES) && loop == 1 ? side_ints_for(c->scene.frames) + (RT_LANE_LDS ? 4 : 0) : 0;
+  // Side slots after the stacks, then the 4 lane ints philox_loop2 keeps in LDS (RT_LANE_LDS)
+  const bool lane_lds = loop >= 1 && (RT_LANE_LDS >= 2 || (RT_LANE_LDS == 1 && is_full(var)));
+  const int side_ints = ((var & F_FRAMES) && loop == 1 ? side_ints_for(c->scene.frames) : 0) + (lane_lds ? 4 : 0);
   // LDS-staged kernel when the traversal's node array plus the stacks fit one CU's 160 KiB
   // (RTAMD_LDS=0 disables it for A/B runs).
   if (!count && !env_off("RTAMD_LDS") && (!is_full(var) || loop)) {
