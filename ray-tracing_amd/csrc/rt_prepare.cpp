@@ -171,22 +171,39 @@ void mixed_wide_trees(PreparedScene& P, const std::vector<rt_node>& host, const 
   const int n = (int)dev.size();
   if (n >= RT_WNODE) return;  // (ids must stay clear of the RT_WNODE tag)
   std::vector<int> roots;
-  std::vector<char> seen(2 * (size_t)n, 0);
-  std::function<void(int, bool)> find = [&](int id, bool in_ord) {
-    if (seen[2 * (size_t)id + in_ord]) return;
-    seen[2 * (size_t)id + in_ord] = 1;
+  // The top `bin` levels of each re-bounded subtree stay binary (exact fp64 box tests, RTAMD_MIXW_BIN,
+  // default 0): the 4-wide trees start below them. lvl: -1 outside re-bounded subtrees, else the binary
+  // levels above this node inside one; kIn: inside a 4-wide tree already.
+  const char* bin_env = std::getenv("RTAMD_MIXW_BIN");
+  const int bin = bin_env ? std::max(0, std::min(8, std::atoi(bin_env))) : 0;
+  constexpr int kIn = 1 << 20;
+  std::vector<char> seen((size_t)n * (bin + 3), 0);
+  auto is_bvh_at = [&](int id) { return (flat[id].type & RT_TYPE_MASK) == RT_NODE_BVH; };
+  std::function<void(int, int)> find = [&](int id, int lvl) {
+    const size_t key = (size_t)id * (bin + 3) + (size_t)(lvl < 0 ? 0 : (lvl >= kIn ? bin + 2 : 1 + std::min(lvl, bin)));
+    if (seen[key]) return;
+    seen[key] = 1;
     const rt_node& x = flat[id];
     const int ty = x.type & RT_TYPE_MASK;
     if (ty == RT_NODE_BVH) {
       const bool ord = (x.c & RT_BVH_ORDERED) != 0;
-      if (ord && !in_ord) roots.push_back(id);
-      find(x.a, in_ord || ord);  // (frames inside re-bounded subtrees hold subtrees of their own)
-      find(x.b, in_ord || ord);
+      int next = lvl;
+      if (ord && lvl < kIn) {
+        const int here = lvl < 0 ? 0 : lvl;
+        if (here >= bin || !is_bvh_at(x.a) || !is_bvh_at(x.b)) {
+          roots.push_back(id);
+          next = kIn;
+        } else {
+          next = here + 1;
+        }
+      }
+      find(x.a, next);  // (frames inside re-bounded subtrees hold subtrees of their own)
+      find(x.b, next);
     } else if ((ty == RT_NODE_TRANSLATE || ty == RT_NODE_ROTATE) && !(x.type & RT_CHAIN_PRIM)) {
-      find(x.a, false);  // a frame: its child starts a new region
+      find(x.a, -1);  // a frame: its child starts a new region
     }
   };
-  find(world, false);
+  find(world, -1);
   if (roots.empty()) return;
   std::vector<rt_wnode> wide;
   std::vector<int> wroot(n, -1), wneed_root(n, 0);
