@@ -38,6 +38,7 @@ extern "C" {
 #define RT_E_NOMEM (-3)     /* allocation failure                                    */
 #define RT_E_UNSUPPORTED (-4)/* scene uses a construct the device path does not take */
 #define RT_E_STATE (-5)     /* call order (e.g. render before upload)                */
+#define RT_E_COMM (-6)      /* RCCL error (multi-device contexts)                    */
 
 /* ------------------------------------------------------------------ scene records */
 
@@ -318,6 +319,40 @@ typedef struct rt_ctx rt_ctx;
 int rt_device_count(int* out);
 /* Bind one HIP device (one process per GPU). */
 int rt_create(int device, rt_ctx** out);
+/*
+ * One context over n_devices GPUs, driven from one host thread ("rt_create(num_gpus)":
+ * the ctx owns the devices and an RCCL communicator over them). devices: n_devices distinct HIP device
+ * ids, or NULL for 0..n_devices-1; at most RT_MAX_DEVICES. RCCL ranks follow the list order.
+ *   rt_upload_scene[_ex]: validates and prepares the scene once, then copies it to every device.
+ *   rt_render, tier B: the image's tiles are dealt round-robin over the devices (shard r = the r-th
+ *     device, the rt_render_shard_async layout with shard_count = n_devices), each device renders its
+ *     slab on its own stream, the slabs are gathered to the first device with RCCL (ncclGather over
+ *     xGMI, grouped over the devices' communicators), which assembles the image and copies it to the
+ *     host. The bytes equal a one-device rt_render of the same params (tier B is shard-invariant).
+ *   rt_render, tier A: the reference's per-column streams are one serial chain per column, so tier A
+ *     does not shard: it renders on the first device.
+ * Every other call on a multi-device ctx (the *_async building blocks, debug entries, counting
+ * renders) acts on its first device. This replaces the reference's only parallelism, the row sparks
+ * of runRender (src/Lib.hs:1519-1520), as called from app/Main.hs:50-58.
+ */
+#define RT_MAX_DEVICES 16
+int rt_create_multi(int n_devices, const int* devices, rt_ctx** out);
+/* Devices of a ctx: *out_n = count; out_devices (may be NULL) receives up to `cap` device ids. */
+int rt_ctx_devices(const rt_ctx* ctx, int* out_n, int* out_devices, int cap);
+/* Timing of the last rt_render on a ctx (HIP events on each device's launch stream), ms:
+ * kernel_ms[r] = device r's render launches (chunk batches included), gather_ms = from the first
+ * device's render end to the end of the RCCL gather on its stream (includes waiting for the slowest
+ * device), assemble_ms = the assemble kernel, frame_ms = first launch to assembled image (before the
+ * device-to-host copy). n_devices = 1 and gather_ms = 0 on a one-device ctx. */
+typedef struct rt_frame_timing {
+    int32_t n_devices;
+    int32_t _pad;
+    double kernel_ms[RT_MAX_DEVICES];
+    double gather_ms;
+    double assemble_ms;
+    double frame_ms;
+} rt_frame_timing;
+int rt_last_frame_timing(rt_ctx* ctx, rt_frame_timing* out);
 void rt_destroy(rt_ctx* ctx);
 /* Copy a scene to device memory (caller-owned desc; arrays are copied). Validates it.
  * By default a world tree without ConstantMedium is re-bounded by a binned-SAH BVH over the same

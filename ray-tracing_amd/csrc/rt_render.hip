@@ -15,8 +15,16 @@
 //  * forward throughput (thr *= att * (spdf / pdf)) instead of the reference's continuation;
 //    colour never feeds control flow or the RNG, so this changes rounding only;
 //  * traversal stacks live in LDS, [entry][lane] so consecutive lanes hit consecutive banks;
-//  * tier B (Philox per (pixel, sample)) shards by tiles with no data-path collective; tier A
-//    (the reference's per-column SplitMix stream) runs one lane per column.
+//  * tier B (Philox per (pixel, sample)) shards by tiles with no data-path collective before the
+//    final framebuffer gather; tier A (the reference's per-column SplitMix stream) runs one lane per
+//    column;
+//  * a multi-device ctx (rt_create_multi) renders one tile shard per GPU from one host thread and
+//    gathers the RGB8 slabs to its first device with RCCL (grouped ncclGather), which assembles.
+#include <rccl/rccl.h>
+
+#include <numeric>
+#include <vector>
+
 #include "rt_kernels.h"
 #include "rt_prepare.h"
 
@@ -60,6 +68,13 @@ struct rt_ctx {
   size_t acc_bytes = 0;
   double last_ms = 0.0;
   rt_launch_info last_launch{};  // rt_last_launch
+  // rt_render's frame events: after the render launches (gather start), after the gather, after assembly
+  hipEvent_t ev_gather = nullptr, ev_gathered = nullptr, ev_asm = nullptr;
+  rt_frame_timing last_frame{};  // rt_last_frame_timing
+  // Multi-device ctx (rt_create_multi): this ctx is the first device's (RCCL rank 0, the gather root);
+  // peers[r - 1] is device r's, comms[r] its communicator (ncclCommInitAll, ranks in list order).
+  std::vector<rt_ctx*> peers;
+  std::vector<ncclComm_t> comms;
 };
 
 namespace {
@@ -68,10 +83,21 @@ int hip_fail(hipError_t e, const char* what) {
   rt::set_error(std::string(what) + ": " + hipGetErrorString(e));
   return RT_E_HIP;
 }
+int hip_ok(hipError_t e, const char* what) { return e == hipSuccess ? RT_OK : hip_fail(e, what); }
 #define HIPCHK(x)                                  \
   do {                                             \
     hipError_t _e = (x);                           \
     if (_e != hipSuccess) return hip_fail(_e, #x); \
+  } while (0)
+
+int nccl_fail(ncclResult_t r, const char* what) {
+  rt::set_error(std::string(what) + ": " + ncclGetErrorString(r));
+  return RT_E_COMM;
+}
+#define NCCLCHK(x)                                    \
+  do {                                                \
+    ncclResult_t _r = (x);                            \
+    if (_r != ncclSuccess) return nccl_fail(_r, #x);  \
   } while (0)
 
 // Device allocation released when it goes out of scope (every return path of the blocking calls).
@@ -416,6 +442,116 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   return run(fn, dim3(grid), dim3(RT_BLOCK), dyn, args);
 }
 
+// Device buffer on a given device (freed with that device selected).
+struct DevBufOn {
+  int dev = -1;
+  void* p = nullptr;
+  DevBufOn() = default;
+  DevBufOn(const DevBufOn&) = delete;
+  DevBufOn& operator=(const DevBufOn&) = delete;
+  ~DevBufOn() {
+    if (!p) return;
+    DeviceGuard _dg(dev);
+    (void)hipFree(p);
+  }
+  int alloc(int device, size_t bytes) {
+    dev = device;
+    DEVICE_SCOPE(device);
+    HIPCHK(hipMalloc(&p, bytes));
+    return RT_OK;
+  }
+};
+
+// rt_render, tier B, on a multi-device ctx (rt_create_multi): shard r of N = the ctx's r-th device. Every
+// device renders its tiles into a slab on its own stream (the launches are queued from this thread and
+// run concurrently); the slabs are gathered to device 0 by RCCL (one ncclGather per communicator, grouped,
+// each on its device's stream after that device's render), which assembles the image.
+// Not in place: device 0 renders into its own slab too, so the gather moves bytes even at N = 1.
+int render_multi(rt_ctx* c, const rt_camera* cam, rt_render_params p, uint8_t* out_rgb, double* out_lin) {
+  const int n = 1 + (int)c->peers.size();
+  p.shard_count = n;
+  int tile, tiles_x;
+  long long tt, ps, slab;
+  geometry(&p, tile, tiles_x, tt, ps, slab);
+  auto dev_ctx = [&](int r) { return r == 0 ? c : c->peers[r - 1]; };
+  const long long npx = (long long)p.width * p.height;
+  std::vector<DevBufOn> send(n), send_lin(n);
+  DevBufOn gathered, gathered_lin, img, img_lin;  // on device 0
+  int rc = RT_OK;
+  for (int r = 0; r < n && !rc; ++r) {
+    rt_ctx* d = dev_ctx(r);
+    if ((rc = send[r].alloc(d->device, (size_t)slab * 3))) break;
+    if (out_lin && (rc = send_lin[r].alloc(d->device, sizeof(double) * (size_t)slab * 3))) break;
+  }
+  if (!rc) rc = gathered.alloc(c->device, (size_t)n * slab * 3);
+  if (!rc && out_lin) rc = gathered_lin.alloc(c->device, sizeof(double) * (size_t)n * slab * 3);
+  if (!rc) rc = img.alloc(c->device, (size_t)npx * 3);
+  if (!rc && out_lin) rc = img_lin.alloc(c->device, sizeof(double) * (size_t)npx * 3);
+  if (rc) return rc;
+  // the shards' renders, one per device, queued back to back
+  for (int r = 0; r < n; ++r) {
+    rt_ctx* d = dev_ctx(r);
+    DEVICE_SCOPE(d->device);
+    rt_render_params pr = p;
+    pr.shard_rank = r;
+    if ((rc = launch_philox(d, cam, &pr, r, n, (uint8_t*)send[r].p, (double*)send_lin[r].p, d->stream))) return rc;
+    if (r == 0) HIPCHK(hipEventRecord(c->ev_gather, c->stream));
+  }
+  // the RCCL gather of the slabs to device 0 (rank 0), in the ranks' stream order after their renders
+  {
+    DeviceGuard _dg(c->device);
+    NCCLCHK(ncclGroupStart());
+    for (int r = 0; r < n; ++r) {
+      rt_ctx* d = dev_ctx(r);
+      const ncclResult_t g = ncclGather(send[r].p, r == 0 ? gathered.p : nullptr, (size_t)slab * 3, ncclUint8, 0,
+                                        c->comms[r], d->stream);
+      const ncclResult_t gl = g == ncclSuccess && out_lin
+                                  ? ncclGather(send_lin[r].p, r == 0 ? gathered_lin.p : nullptr, (size_t)slab * 3,
+                                               ncclFloat64, 0, c->comms[r], d->stream)
+                                  : g;
+      if (gl != ncclSuccess) {
+        (void)ncclGroupEnd();
+        return nccl_fail(gl, "ncclGather");
+      }
+    }
+    NCCLCHK(ncclGroupEnd());
+  }
+  {
+    DEVICE_SCOPE(c->device);
+    HIPCHK(hipEventRecord(c->ev_gathered, c->stream));
+    if ((rc = rt_assemble_async(c, &p, (const uint8_t*)gathered.p, (uint8_t*)img.p, c->stream))) return rc;
+    if (out_lin &&
+        (rc = rt_assemble_linear_async(c, &p, (const double*)gathered_lin.p, (double*)img_lin.p, c->stream)))
+      return rc;
+    HIPCHK(hipEventRecord(c->ev_asm, c->stream));
+  }
+  for (int r = 0; r < n; ++r) {  // (the peers' streams too: their slabs are freed on return)
+    rt_ctx* d = dev_ctx(r);
+    DEVICE_SCOPE(d->device);
+    HIPCHK(hipStreamSynchronize(d->stream));
+  }
+  DEVICE_SCOPE(c->device);
+  HIPCHK(hipMemcpy(out_rgb, img.p, (size_t)npx * 3, hipMemcpyDeviceToHost));
+  if (out_lin) HIPCHK(hipMemcpy(out_lin, img_lin.p, sizeof(double) * (size_t)npx * 3, hipMemcpyDeviceToHost));
+  rt_frame_timing ft{};
+  ft.n_devices = n;
+  float ms = 0;
+  for (int r = 0; r < n; ++r) {
+    rt_ctx* d = dev_ctx(r);
+    HIPCHK(hipEventElapsedTime(&ms, d->ev0, d->ev1));
+    d->last_ms = ms;
+    ft.kernel_ms[r] = ms;
+  }
+  HIPCHK(hipEventElapsedTime(&ms, c->ev_gather, c->ev_gathered));
+  ft.gather_ms = ms;
+  HIPCHK(hipEventElapsedTime(&ms, c->ev_gathered, c->ev_asm));
+  ft.assemble_ms = ms;
+  HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev_asm));
+  ft.frame_ms = ms;
+  c->last_frame = ft;
+  return RT_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -446,6 +582,9 @@ int rt_create(int device, rt_ctx** out) {
     HIPCHK(hipEventCreate(&c->ev0));
     HIPCHK(hipEventCreate(&c->ev1));
     HIPCHK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
+    HIPCHK(hipEventCreate(&c->ev_gather));
+    HIPCHK(hipEventCreate(&c->ev_gathered));
+    HIPCHK(hipEventCreate(&c->ev_asm));
     HIPCHK(hipMalloc((void**)&c->d_counter, 256));
     return RT_OK;
   };
@@ -458,8 +597,69 @@ int rt_create(int device, rt_ctx** out) {
   return RT_OK;
 }
 
+int rt_create_multi(int n, const int* devices, rt_ctx** out) {
+  if (!out) return invalid("null out");
+  *out = nullptr;
+  if (n < 1 || n > RT_MAX_DEVICES) return invalid("n_devices must be in [1, RT_MAX_DEVICES]");
+  int avail = 0;
+  HIPCHK(hipGetDeviceCount(&avail));
+  std::vector<int> list(n);
+  if (devices) std::copy(devices, devices + n, list.begin());
+  else std::iota(list.begin(), list.end(), 0);
+  for (int i = 0; i < n; ++i) {
+    if (list[i] < 0 || list[i] >= avail) return invalid("device index out of range");
+    for (int j = 0; j < i; ++j)
+      if (list[j] == list[i]) return invalid("device listed twice (one RCCL rank per GPU)");
+  }
+  rt_ctx* c = nullptr;
+  int rc = rt_create(list[0], &c);
+  if (rc) return rc;
+  for (int i = 1; i < n && !rc; ++i) {
+    rt_ctx* p = nullptr;
+    rc = rt_create(list[i], &p);
+    if (!rc) c->peers.push_back(p);
+  }
+  if (!rc) {
+    DeviceGuard _dg(list[0]);  // (ncclCommInitAll selects each device in turn; the caller's is restored)
+    c->comms.assign(n, nullptr);
+    const ncclResult_t r = ncclCommInitAll(c->comms.data(), n, list.data());
+    if (r != ncclSuccess) {
+      c->comms.clear();
+      rc = nccl_fail(r, "ncclCommInitAll");
+    }
+  }
+  if (rc) {
+    rt_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return RT_OK;
+}
+
+int rt_ctx_devices(const rt_ctx* c, int* out_n, int* out_devices, int cap) {
+  if (!c || !out_n || cap < 0) return invalid("null argument");
+  *out_n = 1 + (int)c->peers.size();
+  for (int r = 0; out_devices && r < *out_n && r < cap; ++r)
+    out_devices[r] = r == 0 ? c->device : c->peers[r - 1]->device;
+  return RT_OK;
+}
+
+int rt_last_frame_timing(rt_ctx* c, rt_frame_timing* out) {
+  if (!c || !out) return invalid("null argument");
+  *out = c->last_frame;
+  return RT_OK;
+}
+
 void rt_destroy(rt_ctx* c) {
   if (!c) return;
+  for (size_t r = 0; r < c->comms.size(); ++r) {
+    if (!c->comms[r]) continue;
+    DeviceGuard _dr(r == 0 ? c->device : c->peers[r - 1]->device);
+    (void)ncclCommDestroy(c->comms[r]);
+  }
+  c->comms.clear();
+  for (rt_ctx* p : c->peers) rt_destroy(p);
+  c->peers.clear();
   DeviceGuard _dg(c->device);
   free_scene(c);
   (void)hipFree(c->d_counter);
@@ -468,6 +668,9 @@ void rt_destroy(rt_ctx* c) {
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ev_done) (void)hipEventDestroy(c->ev_done);
+  if (c->ev_gather) (void)hipEventDestroy(c->ev_gather);
+  if (c->ev_gathered) (void)hipEventDestroy(c->ev_gathered);
+  if (c->ev_asm) (void)hipEventDestroy(c->ev_asm);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -475,12 +678,12 @@ void rt_destroy(rt_ctx* c) {
 
 int rt_upload_scene(rt_ctx* c, const rt_scene_desc* d) { return rt_upload_scene_ex(c, d, 0u); }
 
-int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
-  if (!c || !din) return invalid("null argument");
-  // the host half (rt_prepare.cpp): validation, the walk's trees, the tagged device copy
-  rt::PreparedScene P;
-  int rc = rt::prepare_scene(din, flags, P);
-  if (rc) return rc;
+}  // extern "C"
+
+namespace {
+// Copies a prepared scene to c's device (replacing its scene).
+int upload_prepared(rt_ctx* c, const rt::PreparedScene& P, const rt_scene_desc* din) {
+  int rc = RT_OK;
   DEVICE_SCOPE(c->device);
   free_scene(c);
   if ((rc = upload(&c->d_nodes, P.nodes.data(), P.nodes.size())) ||
@@ -522,6 +725,29 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
   c->replace_ok = P.replace_ok;
   c->has_scene = true;
   return RT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int rt_upload_scene_ex(rt_ctx* c, const rt_scene_desc* din, uint32_t flags) {
+  if (!c || !din) return invalid("null argument");
+  // the host half (rt_prepare.cpp): validation, the walk's trees, the tagged device copy — once, then
+  // the copy goes to every device of the ctx (a malformed descriptor leaves every device's scene as it was)
+  rt::PreparedScene P;
+  int rc = rt::prepare_scene(din, flags, P);
+  if (rc) return rc;
+  rc = upload_prepared(c, P, din);
+  for (size_t r = 0; r < c->peers.size() && !rc; ++r) rc = upload_prepared(c->peers[r], P, din);
+  if (rc) {  // (a device failed: no device keeps a scene, so a multi-device render cannot mix two)
+    for (rt_ctx* p : c->peers) {
+      DeviceGuard _dg(p->device);
+      free_scene(p);
+    }
+    DeviceGuard _dg(c->device);
+    free_scene(c);
+  }
+  return rc;
 }
 
 int rt_shard_geometry(const rt_render_params* p, int64_t* tiles_total, int64_t* tiles_per_shard,
@@ -596,6 +822,12 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, cons
     return RT_E_STATE;
   }
   if (p.rng_mode == RT_RNG_EXACT && !col_gens) return invalid("rt_render: tier A needs col_gens (2*width words)");
+  for (rt_ctx* q : c->peers)
+    if (!q->has_scene) {
+      rt::set_error("rt_render: no scene uploaded on every device");
+      return RT_E_STATE;
+    }
+  if (p.rng_mode == RT_RNG_PHILOX && !c->comms.empty()) return render_multi(c, cam, p, out_rgb, out_lin);
   DEVICE_SCOPE(c->device);
   const long long npx = (long long)p.width * p.height;
   hipStream_t st = c->stream;
@@ -604,6 +836,8 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, cons
   if (out_lin) HIPCHK(hipMalloc(&img_lin.p, sizeof(double) * (size_t)npx * 3));
   uint8_t* d_img = (uint8_t*)img.p;
   double* d_img_lin = (double*)img_lin.p;
+  rt_frame_timing ft{};
+  ft.n_devices = 1;
   if (p.rng_mode == RT_RNG_PHILOX) {
     int tile, tiles_x;
     long long tt, ps, slab;
@@ -611,10 +845,17 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, cons
     HIPCHK(hipMalloc(&slab_buf.p, (size_t)slab * 3));
     if (out_lin) HIPCHK(hipMalloc(&slab_lin.p, sizeof(double) * (size_t)slab * 3));
     rc = launch_philox(c, cam, &p, 0, 1, (uint8_t*)slab_buf.p, (double*)slab_lin.p, st);
+    if (!rc) rc = hip_ok(hipEventRecord(c->ev_gather, st), "hipEventRecord");
     if (!rc) rc = rt_assemble_async(c, &p, (const uint8_t*)slab_buf.p, d_img, st);
     if (!rc && out_lin) rc = rt_assemble_linear_async(c, &p, (const double*)slab_lin.p, d_img_lin, st);
+    if (!rc) rc = hip_ok(hipEventRecord(c->ev_asm, st), "hipEventRecord");
     HIPCHK(hipStreamSynchronize(st));
     if (rc) return rc;
+    float a = 0, f = 0;
+    HIPCHK(hipEventElapsedTime(&a, c->ev_gather, c->ev_asm));
+    HIPCHK(hipEventElapsedTime(&f, c->ev0, c->ev_asm));
+    ft.assemble_ms = a;
+    ft.frame_ms = f;
   } else {
     HIPCHK(hipMalloc(&gens.p, sizeof(uint64_t) * 2 * (size_t)p.width));
     uint64_t* d_gens = (uint64_t*)gens.p;
@@ -643,6 +884,9 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, cons
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
   c->last_ms = ms;
+  ft.kernel_ms[0] = ms;
+  if (p.rng_mode == RT_RNG_EXACT) ft.frame_ms = ms;
+  c->last_frame = ft;
   return RT_OK;
 }
 

@@ -46,7 +46,8 @@ PROBE_OUT = (14, 4, 2, 3, 8)
 
 XYPlane, XZPlane, YZPlane = 0, 1, 2
 XAxis, YAxis, ZAxis = 0, 1, 2
-RT_OK, RT_E_INVALID, RT_E_HIP, RT_E_NOMEM, RT_E_UNSUPPORTED, RT_E_STATE = 0, -1, -2, -3, -4, -5
+RT_OK, RT_E_INVALID, RT_E_HIP, RT_E_NOMEM, RT_E_UNSUPPORTED, RT_E_STATE, RT_E_COMM = 0, -1, -2, -3, -4, -5, -6
+RT_MAX_DEVICES = 16
 
 SCENES = {
     "cornell": 0, "cornell_smoke": 1, "simple_light": 2, "earth": 3, "two_perlin_spheres": 4,
@@ -106,6 +107,11 @@ class rt_scene_info(C.Structure):
         (n, C.c_int32) for n in ("rebuilt_bvh", "mixed_wide", "replace_ok", "ref_walk")]
 
 
+class rt_frame_timing(C.Structure):
+    _fields_ = [("n_devices", C.c_int32), ("_pad", C.c_int32), ("kernel_ms", C.c_double * RT_MAX_DEVICES),
+                ("gather_ms", C.c_double), ("assemble_ms", C.c_double), ("frame_ms", C.c_double)]
+
+
 class rt_render_params(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_int32), ("max_depth", C.c_int32),
                 ("rng_mode", C.c_int32), ("flags", C.c_uint32), ("seed", C.c_uint64), ("tile", C.c_int32),
@@ -128,7 +134,7 @@ EXPORTED = [
     "rt_render_shard_async", "rt_assemble_async", "rt_assemble_linear_async", "rt_last_kernel_ms",
     "rt_debug_closest_hits", "rt_debug_math", "rt_render_work", "rt_upload_scene_ex", "rt_rebuild_bvh",
     "rt_wide_bvh", "rt_tree_stack_need", "rt_last_launch", "rt_write_pfm", "rt_debug_probe",
-    "rt_prepare_scene", "rt_render_step_profile",
+    "rt_prepare_scene", "rt_render_step_profile", "rt_create_multi", "rt_ctx_devices", "rt_last_frame_timing",
 ]
 
 # include/rt_wide.h: one 4-wide node (128 B)
@@ -150,6 +156,9 @@ def _share_torch_hip_runtime():
     spec = importlib.util.find_spec("torch")
     if spec is None or not spec.origin:
         return
+    # (RCCL, which librtamd.so links for the multi-device gather, is not preloaded this way: torch's
+    # librccl.so carries /opt/rocm's soname librccl.so.1, so the process maps one RCCL whichever library
+    # is loaded first, and preloading torch's copy globally aborts the interpreter at exit)
     hip = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
     if os.path.exists(hip):
         C.CDLL(hip, mode=C.RTLD_GLOBAL)
@@ -209,6 +218,9 @@ def lib() -> C.CDLL:
             "rt_debug_probe": (I, [C.c_void_p, P(rt_camera), I, P(D), I, U64, P(D)]),
             "rt_prepare_scene": (I, [P(rt_scene_desc), C.c_uint32, P(rt_scene_info)]),
             "rt_render_step_profile": (I, [C.c_void_p, P(rt_camera), P(rt_render_params), P(U64), P(U64)]),
+            "rt_create_multi": (I, [I, P(I), P(C.c_void_p)]),
+            "rt_ctx_devices": (I, [C.c_void_p, P(I), P(I), I]),
+            "rt_last_frame_timing": (I, [C.c_void_p, P(rt_frame_timing)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -478,14 +490,36 @@ def device_count() -> int:
 
 
 class Context:
-    """One HIP device (one process per GPU)."""
+    """One HIP device (one process per GPU), or with `devices`, one context over several GPUs driven
+    from this thread (rt_create_multi: tier-B renders are tile-sharded over the devices and gathered
+    to the first with RCCL)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, devices: Optional[Sequence[int]] = None):
         h = C.c_void_p()
-        _check(lib().rt_create(device, C.byref(h)), "rt_create")
+        if devices is None:
+            _check(lib().rt_create(device, C.byref(h)), "rt_create")
+        else:
+            devs = (C.c_int * len(devices))(*devices)
+            _check(lib().rt_create_multi(len(devices), devs, C.byref(h)), "rt_create_multi")
+            device = int(devices[0])
         self._h = h
         self.device = device
         self._scene = None
+
+    def devices(self) -> List[int]:
+        """rt_ctx_devices: the ctx's HIP devices (RCCL rank order)."""
+        n = C.c_int(0)
+        out = (C.c_int * RT_MAX_DEVICES)()
+        _check(lib().rt_ctx_devices(self._h, C.byref(n), out, RT_MAX_DEVICES), "rt_ctx_devices")
+        return [int(out[i]) for i in range(n.value)]
+
+    def frame_timing(self) -> dict:
+        """rt_last_frame_timing: per-device render kernel ms, RCCL gather ms, assemble ms, frame ms of the
+        last rt_render."""
+        t = rt_frame_timing()
+        _check(lib().rt_last_frame_timing(self._h, C.byref(t)), "rt_last_frame_timing")
+        return {"n_devices": t.n_devices, "kernel_ms": [t.kernel_ms[i] for i in range(t.n_devices)],
+                "gather_ms": t.gather_ms, "assemble_ms": t.assemble_ms, "frame_ms": t.frame_ms}
 
     def close(self):
         if self._h is not None:

@@ -22,11 +22,13 @@ class ShardedFrame:
 
     device: a torch device ("cuda:k" on the GPU box, "cpu" for gloo rehearsals and tests).
     backend: "nccl" (device all-gather) or "gloo" (host-staged all-gather).
+    gather: run the all-gather through the process group (default: when world > 1). True at world 1
+    exercises the collective path on one GPU (the slabs then round-trip through RCCL).
     """
 
     def __init__(self, params, world: int, rank: int, device, backend: str = "nccl",
                  render: Optional[Callable] = None, assemble: Optional[Callable] = None,
-                 stream=None):
+                 stream=None, gather: Optional[bool] = None):
         import torch
 
         import rtamd
@@ -43,6 +45,7 @@ class ShardedFrame:
         self.stream = stream
         self._render = render
         self._assemble = assemble
+        self.gather = world > 1 if gather is None else bool(gather)
         self.timings: List[dict] = []  # per step: kernel / all-gather / assemble (ms), filled by finish()
         self._ev: List[tuple] = []
 
@@ -54,7 +57,7 @@ class ShardedFrame:
         self._render(self.p, self.slab)
         if ev:
             ev[0].record()
-        if self.world > 1:
+        if self.gather:
             import torch.distributed as dist
             if self.backend == "nccl":
                 dist.all_gather_into_tensor(self.slabs, self.slab)  # RCCL over xGMI

@@ -10,10 +10,17 @@
  * way from its roots, then:
  *   CPU: checks the re-flattened descriptor is well formed for the library (rt_rebuild_bvh,
  *        rt_tree_stack_need) and that the duplication is what the Haskell module produces;
- *   GPU (argv[1] == "gpu"): runs runRenderAMD's sequence — rt_create, rt_upload_scene, rt_render in
- *        tier A with one (seed, gamma) per column (the deterministic app/Main.hs:47-49 harness:
- *        column 0 = the builder's g1, column x = randGen (1024 + x)), rt_destroy — and checks the bytes
- *        and end-of-stream generators equal those of the builder's own descriptor; tier B too.
+ *   GPU (argv[1] == "gpu"): runs runRenderAMD's sequence — rt_create_multi over every visible GPU
+ *        (RenderAMD's default: the tile shards of a tier-B frame spread over the devices and gathered
+ *        with RCCL), rt_upload_scene, rt_render in tier A with one (seed, gamma) per column (the
+ *        deterministic app/Main.hs:47-49 harness: column 0 = the builder's g1, column x = randGen
+ *        (1024 + x)) and in tier B, rt_destroy — and checks the bytes and end-of-stream generators equal
+ *        those of the builder's own descriptor rendered on one device (rt_create). With argv[2] = a
+ *        directory, it also writes <dir>/<scene>.bin: the flattened descriptor, the column generators
+ *        and both tiers' outputs (RGB8, linear averages, tier-A end generators), which
+ *        tests/test_ffi_sequence.py renders with the CPU oracle from the same flattened records.
+ *   CPU, argv = "dump <dir>": writes the same files with zero outputs (the flattening checked on the
+ *        CPU: the oracle renders the flattened records as it renders the builder's).
  * Exit 0 on success; prints one line per scene.
  */
 #include <stdint.h>
@@ -117,12 +124,40 @@ static int flat_hit(Flat* f, int id) {
   return f->n - 1;
 }
 
+/* <dir>/<name>.bin (little-endian, native structs): "RTFS" v1; W H spp depth; n_nodes n_materials
+   n_textures n_perlins n_images world lights; pool_bytes (i64); background[3]; the arrays; col gens
+   (2W u64); tier A rgb8, linear (H*W*3 f64), end gens; tier B rgb8, linear */
+static int dump(const char* dir, const char* name, const rt_scene_desc* d, int W, int H, int spp, int depth,
+                const uint64_t* gens, const uint8_t* rgb_a, const double* lin_a, const uint64_t* go_a,
+                const uint8_t* rgb_b, const double* lin_b) {
+  char path[4096];
+  snprintf(path, sizeof path, "%s/%s.bin", dir, name);
+  FILE* f = fopen(path, "wb");
+  if (!f) return 1;
+  const int32_t hdr[13] = {0x53465452, 1, W, H, spp, depth, d->n_nodes, d->n_materials, d->n_textures,
+                           d->n_perlins, d->n_images, d->world_root, d->lights_root};
+  const size_t px = (size_t)W * H * 3;
+  int ok = fwrite(hdr, sizeof hdr, 1, f) == 1 && fwrite(&d->image_pool_bytes, 8, 1, f) == 1 &&
+           fwrite(d->background, 8, 3, f) == 3 &&
+           fwrite(d->nodes, sizeof(rt_node), (size_t)d->n_nodes, f) == (size_t)d->n_nodes &&
+           fwrite(d->materials, sizeof(rt_material), (size_t)d->n_materials, f) == (size_t)d->n_materials &&
+           fwrite(d->textures, sizeof(rt_texture), (size_t)d->n_textures, f) == (size_t)d->n_textures &&
+           fwrite(d->perlins, sizeof(rt_perlin), (size_t)d->n_perlins, f) == (size_t)d->n_perlins &&
+           fwrite(d->images, sizeof(rt_image), (size_t)d->n_images, f) == (size_t)d->n_images &&
+           fwrite(d->image_pool, 1, (size_t)d->image_pool_bytes, f) == (size_t)d->image_pool_bytes &&
+           fwrite(gens, 8, 2 * (size_t)W, f) == 2 * (size_t)W && fwrite(rgb_a, 1, px, f) == px &&
+           fwrite(lin_a, 8, px, f) == px && fwrite(go_a, 8, 2 * (size_t)W, f) == 2 * (size_t)W &&
+           fwrite(rgb_b, 1, px, f) == px && fwrite(lin_b, 8, px, f) == px;
+  ok = fclose(f) == 0 && ok;
+  return !ok;
+}
+
 static int fail(const char* what) {
   fprintf(stderr, "FAIL %s: %s\n", what, rt_last_error());
   return 1;
 }
 
-static int run(int scene_id, const char* name, int cam_id, int W, int H, int spp, int gpu) {
+static int run(int scene_id, const char* name, int cam_id, int W, int H, int spp, int gpu, const char* dir) {
   uint64_t g[2];
   rt_rand_gen(1024, g);
   rt_builder* b;
@@ -178,23 +213,36 @@ static int run(int scene_id, const char* name, int cam_id, int W, int H, int spp
   if (gpu) {
     rt_camera cam;
     if (rt_camera_named(cam_id, W, H, &cam)) return fail("rt_camera_named");
+    int ndev = 0;
+    if (rt_device_count(&ndev) || ndev < 1) return fail("rt_device_count");
+    if (ndev > RT_MAX_DEVICES) ndev = RT_MAX_DEVICES;
     uint64_t* gens = malloc(sizeof(uint64_t) * 2 * (size_t)W);
     gens[0] = g1[0];
     gens[1] = g1[1];
     for (int x = 1; x < W; ++x) rt_rand_gen(1024 + x, gens + 2 * x);
-    uint8_t *rgb_a = malloc((size_t)W * H * 3), *rgb_d = malloc((size_t)W * H * 3);
+    const size_t px = (size_t)W * H * 3;
+    uint8_t *rgb_a = malloc(px), *rgb_d[2] = {malloc(px), malloc(px)};
+    double* lin_d[2] = {malloc(px * 8), malloc(px * 8)};
     uint64_t *go_a = malloc(sizeof(uint64_t) * 2 * (size_t)W), *go_d = malloc(sizeof(uint64_t) * 2 * (size_t)W);
     for (int tier = 0; tier < 2 && !rc; ++tier) {
       rt_render_params p = {W, H, spp, 50, tier ? RT_RNG_PHILOX : RT_RNG_EXACT, 0, 1024, 16, 0, 1, 0};
       for (int which = 0; which < 2 && !rc; ++which) {
-        rt_ctx* ctx; /* runRenderAMD: rt_create, rt_upload_scene, rt_render, rt_destroy */
-        if (rt_create(0, &ctx)) return fail("rt_create");
+        /* runRenderAMD: rt_create_multi, rt_upload_scene, rt_render, rt_destroy (the builder's own
+           descriptor on one device: rt_create) */
+        rt_ctx* ctx;
+        if (which ? rt_create_multi(ndev, NULL, &ctx) : rt_create(0, &ctx))
+          return fail(which ? "rt_create_multi" : "rt_create");
         if (rt_upload_scene(ctx, which ? &d : &a)) rc = fail("rt_upload_scene");
-        else if (rt_render(ctx, &cam, &p, gens, which ? rgb_d : rgb_a, NULL, which ? go_d : go_a))
+        else if (rt_render(ctx, &cam, &p, gens, which ? rgb_d[tier] : rgb_a, which ? lin_d[tier] : NULL,
+                           which ? go_d : go_a))
           rc = fail("rt_render");
+        if (!rc && which && tier) {
+          rt_frame_timing t;
+          if (rt_last_frame_timing(ctx, &t) || t.n_devices != ndev) rc = fail("rt_last_frame_timing");
+        }
         rt_destroy(ctx);
       }
-      if (!rc && memcmp(rgb_a, rgb_d, (size_t)W * H * 3)) {
+      if (!rc && memcmp(rgb_a, rgb_d[tier], px)) {
         fprintf(stderr, "FAIL %s: tier %c bytes differ\n", name, tier ? 'B' : 'A');
         rc = 1;
       }
@@ -203,8 +251,26 @@ static int run(int scene_id, const char* name, int cam_id, int W, int H, int spp
         rc = 1;
       }
     }
-    if (!rc) printf(", GPU tier A + B %dx%dx%d: identical bytes and end generators", W, H, spp);
-    free(gens), free(rgb_a), free(rgb_d), free(go_a), free(go_d);
+    if (!rc) printf(", GPU tier A + B %dx%dx%d on %d device(s): identical bytes and end generators", W, H, spp, ndev);
+    if (!rc && dir && dump(dir, name, &d, W, H, spp, 50, gens, rgb_d[0], lin_d[0], go_a, rgb_d[1], lin_d[1])) {
+      fprintf(stderr, "FAIL %s: cannot write %s/%s.bin\n", name, dir, name);
+      rc = 1;
+    }
+    free(gens), free(rgb_a), free(rgb_d[0]), free(rgb_d[1]), free(lin_d[0]), free(lin_d[1]), free(go_a), free(go_d);
+  }
+  if (!gpu && dir) { /* "dump" mode (no GPU): the flattened records and the generators, zero outputs */
+    const size_t px = (size_t)W * H * 3;
+    uint64_t* gens = calloc(2 * (size_t)W, sizeof(uint64_t));
+    gens[0] = g1[0];
+    gens[1] = g1[1];
+    for (int x = 1; x < W; ++x) rt_rand_gen(1024 + x, gens + 2 * x);
+    uint8_t* z8 = calloc(px, 1);
+    double* zd = calloc(px, sizeof(double));
+    if (dump(dir, name, &d, W, H, spp, 50, gens, z8, zd, gens, z8, zd)) {
+      fprintf(stderr, "FAIL %s: cannot write %s/%s.bin\n", name, dir, name);
+      rc = 1;
+    }
+    free(gens), free(z8), free(zd);
   }
   printf("\n");
   free(f.nodes), free(f.mats), free(f.texs), free(f.perlins), free(f.images), free(f.pool);
@@ -214,10 +280,12 @@ static int run(int scene_id, const char* name, int cam_id, int W, int H, int spp
 
 int main(int argc, char** argv) {
   const int gpu = argc > 1 && !strcmp(argv[1], "gpu");
+  /* "gpu [dir]" renders (and dumps); "dump dir" only writes the flattened records (CPU) */
+  const char* dir = argc > 2 && (gpu || !strcmp(argv[1], "dump")) ? argv[2] : NULL;
   int rc = 0;
-  rc |= run(RT_SCENE_CORNELL_BOX, "cornell", RT_CAM_CORNELL, 40, 40, 4, gpu);
-  rc |= run(RT_SCENE_NEXT_WEEK_FINAL, "next_week_final", RT_CAM_NEXT_WEEK, 32, 24, 2, gpu);
-  rc |= run(RT_SCENE_RANDOM, "random", RT_CAM_RANDOM_SCENE, 40, 24, 2, gpu);
-  rc |= run(RT_SCENE_CORNELL_SMOKE, "cornell_smoke", RT_CAM_CORNELL, 32, 32, 2, gpu);
+  rc |= run(RT_SCENE_CORNELL_BOX, "cornell", RT_CAM_CORNELL, 40, 40, 4, gpu, dir);
+  rc |= run(RT_SCENE_NEXT_WEEK_FINAL, "next_week_final", RT_CAM_NEXT_WEEK, 32, 24, 2, gpu, dir);
+  rc |= run(RT_SCENE_RANDOM, "random", RT_CAM_RANDOM_SCENE, 40, 24, 2, gpu, dir);
+  rc |= run(RT_SCENE_CORNELL_SMOKE, "cornell_smoke", RT_CAM_CORNELL, 32, 32, 2, gpu, dir);
   return rc;
 }

@@ -39,6 +39,7 @@ def test_struct_sizes_match_header():
     assert C.sizeof(rtamd.rt_launch_info) == 56
     assert rtamd.rt_launch_info.wide_nodes.offset == 44  # (round 3: was _pad)
     assert rtamd.rt_launch_info.chunk_batches.offset == 48  # (round 4)
+    assert C.sizeof(rtamd.rt_frame_timing) == 8 + 8 * rtamd.RT_MAX_DEVICES + 24  # (round 5)
 
 
 def test_param_validation_without_gpu():
@@ -85,6 +86,24 @@ def test_render_without_device_fails_loudly():
         pytest.skip("GPU present")
     with pytest.raises(rtamd.RTError):
         rtamd.Context(0)
+
+
+def test_multi_device_ctx_validation_without_gpu():
+    """rt_create_multi checks its device list before touching a device: 1..RT_MAX_DEVICES devices; with
+    no GPU it fails loudly like rt_create (no CPU fallback). The library links RCCL for the gather."""
+    L = rtamd.lib()
+    h = C.c_void_p()
+    for n in (0, -1, rtamd.RT_MAX_DEVICES + 1):
+        assert L.rt_create_multi(n, None, C.byref(h)) == rtamd.RT_E_INVALID and not h.value
+    import torch
+    if not torch.cuda.is_available():
+        assert L.rt_create_multi(1, None, C.byref(h)) < 0 and not h.value
+        with pytest.raises(rtamd.RTError):
+            rtamd.Context(devices=[0])
+    assert L.rt_ctx_devices(None, None, None, 0) == rtamd.RT_E_INVALID
+    import subprocess
+    ldd = subprocess.run(["ldd", rtamd.LIB_PATH], capture_output=True, text=True).stdout
+    assert "librccl.so.1" in ldd
 
 
 def test_pfm_float_dump_round_trip():

@@ -55,7 +55,7 @@ def test_gloo_two_ranks_gather():
     assert q.get(timeout=5) is True
 
 
-def _frame_worker(rank, world, port, W, H, tile, q):
+def _frame_worker(rank, world, port, W, H, tile, q, gather=None):
     """bench.py's step through rtamd.frame.ShardedFrame on the CPU: the renderer fills the rank's
     slab from a reference image through the shard map (as rt_render_shard_async lays it out), the
     slabs are all-gathered over gloo, rank 0 assembles with the assemble kernel's host restatement."""
@@ -80,7 +80,7 @@ def _frame_worker(rank, world, port, W, H, tile, q):
         slab.copy_(torch.from_numpy(s))
         calls.append(params.shard_rank)
 
-    f = ShardedFrame(p, world, rank, "cpu", backend="gloo", render=render, assemble=host_assembler())
+    f = ShardedFrame(p, world, rank, "cpu", backend="gloo", render=render, assemble=host_assembler(), gather=gather)
     for _ in range(2):
         f.step()
     t = f.finish()
@@ -106,3 +106,16 @@ def test_gloo_sharded_frame_steps():
     assert all(p.exitcode == 0 for p in procs)
     res = dict(q.get(timeout=5) for _ in range(world))
     assert all(res.values()), res
+
+
+def test_gloo_sharded_frame_world_one_gathers():
+    """gather=True at world size 1 runs the collective (the path the GPU suite runs over RCCL with a
+    world-size-1 nccl group) and still assembles the image."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    proc = ctx.Process(target=_frame_worker, args=(0, 1, port, 97, 61, 16, q, True))
+    proc.start()
+    proc.join(120)
+    assert proc.exitcode == 0
+    assert q.get(timeout=5) == (0, True)

@@ -97,6 +97,31 @@ def test_cornell_tier_a(gpu_ctx):
     assert np.array_equal(gens_g, gens_o)
 
 
+@pytest.mark.parametrize("name,camname,w,h,spp", [
+    ("cornell_smoke", "cornell", 40, 40, 4),        # ConstantMedium draws inside the walk (Lib.hs:1053-1080)
+    ("next_week_final", "next_week", 48, 48, 3),    # media, motion blur, Perlin marble, the earth raster
+    ("random", "random_scene", 64, 40, 3),          # moving spheres: the time draw (Lib.hs:1106-1108, 1253-1267)
+    ("random_book_one", "random_scene", 80, 48, 4),  # the bench scene (C2)
+    ("two_perlin_spheres", "two_spheres", 48, 32, 4),
+    ("earth", "two_spheres", 48, 32, 4),
+    ("simple_light", "two_spheres", 48, 32, 4)])
+def test_tier_a_rng_consuming_features(gpu_ctx, name, camname, w, h, spp):
+    """Tier A (RT_RNG_EXACT, the drop-in runRenderAMD's mode: the reference's per-column SplitMix streams)
+    against the oracle on every feature that consumes draws: medium draws interleaved with the walk
+    (Lib.hs:1053-1080), the motion-blur time draw (Lib.hs:1253-1267, 1106-1108), Isotropic's rejection
+    draws (Lib.hs:861-865), Perlin and image textures. The end-of-stream generators count every column's
+    draws: they must be equal."""
+    earth = np.load(_earth_path())["rgb"] if name in ("earth", "random", "next_week_final") else None
+    sc, g1 = _scene(name, earth=earth)
+    cam = rtamd.camera(camname, w, h)
+    gens = rtamd.column_gens(g1, w)
+    p = rtamd.make_params(w, h, spp, 50, rtamd.RT_RNG_EXACT)
+    _, _, gens_g, gens_o = _cmp(gpu_ctx, sc, cam, p, col_gens=gens, what=f"{name} tier A")
+    eq = (gens_g == gens_o).all(axis=1).mean()
+    print(f"{name} tier A: end generators equal in {eq:.6f} of columns")
+    assert np.array_equal(gens_g, gens_o)
+
+
 @pytest.mark.parametrize("name,camname", [("cornell_smoke", "cornell"), ("simple_light", "two_spheres"),
                                           ("two_perlin_spheres", "two_spheres"), ("two_spheres", "two_spheres"),
                                           ("earth", "two_spheres"), ("random", "random_scene"),
