@@ -210,6 +210,12 @@ static inline int rt_sample_chunk(int64_t pixels, int spp) {
                                light-mixture quirk makes most pixels of the bench frames NaN (C2 mid
                                rows, all of C4 at 1000 spp); with this flag the same launches carry
                                every sample's finite colour to a comparable output. */
+#define RT_FLAG_SHARED_LIBM 8u /* tier A only, parity aid: sin, cos, log, atan, asin (and x ** 5) from the
+                               portable include/rt_libm.h instead of the device's OCML, the functions the
+                               oracle evaluates in the same mode. A column's tier-A stream is one serial
+                               chain, so a last-bit difference between two libms that flips any later branch
+                               changes the rest of the column; with one libm on both sides the streams are
+                               compared bit for bit on every scene. */
 
 typedef struct rt_render_params {
     int32_t width;
@@ -507,7 +513,8 @@ int rt_debug_probe(rt_ctx* ctx, const rt_camera* cam, int op, const double* in, 
  * Debug / numerics probe: out[i] = op(x[i], y[i]) evaluated on the device.
  * ops: 0 x/y (IEEE), 1 div_exact(x, y) (reciprocal + Markstein), 2 sqrt x, 3 sin x, 4 cos x,
  * 5 atan x, 6 asin x, 7 log x, 8 pow(x, y), 9 GHC atan2(x, y), 10 tan x, 11 the render path's
- * x ** 5 (schlick; double-double, correctly rounded).
+ * x ** 5 (schlick; double-double, correctly rounded); 12-16 include/rt_libm.h's sin, cos, atan, asin,
+ * log x and 17 GHC atan2(x, y) over them (RT_FLAG_SHARED_LIBM).
  */
 int rt_debug_math(rt_ctx* ctx, int op, const double* x, const double* y, int n, double* out);
 

@@ -15,6 +15,12 @@
  * splitmix-0.1 / random-1.2.0 (stack.yaml:42-44) is UNPINNED against GHC; parity with the
  * reference image is pinned only STATISTICALLY, against the reference-rendered
  * cornellBox1000.png (block means; tests/golden/cornell1000_blocks.npz).
+ *
+ * libm: glibc's sin/cos/log/atan/asin/pow by default (the reference's). With RT_FLAG_SHARED_LIBM in
+ * the render params (tier A parity aid), the portable include/rt_libm.h functions instead, which the
+ * device evaluates bit-identically in that mode (a tier-A column is one serial stream, so one ulp of
+ * libm difference that later flips a branch changes the rest of the column). The mode is a process-wide
+ * switch set for the duration of oracle_render_rows (renders are not run concurrently by the tests).
  */
 #include <math.h>
 #include <stdint.h>
@@ -25,9 +31,19 @@
 #endif
 
 #include "../include/rt.h"
+#include "../include/rt_libm.h"
 
 #define EPSILON 0.0001 /* src/Lib.hs:76-77 */
 static const double PI = 3.141592653589793; /* GHC `pi` for Double */
+
+/* ------------------------------------------------------------------ libm (glibc, or rt_libm.h) */
+static int g_shared_libm = 0;
+static inline double o_sin(double x) { return g_shared_libm ? rtlm_sin(x) : sin(x); }
+static inline double o_cos(double x) { return g_shared_libm ? rtlm_cos(x) : cos(x); }
+static inline double o_log(double x) { return g_shared_libm ? rtlm_log(x) : log(x); }
+static inline double o_atan(double x) { return g_shared_libm ? rtlm_atan(x) : atan(x); }
+static inline double o_asin(double x) { return g_shared_libm ? rtlm_asin(x) : asin(x); }
+static inline double o_pow5(double x) { return g_shared_libm ? rtlm_pow5(x) : pow(x, 5); }
 
 /* ------------------------------------------------------------------ Vec3 (src/Lib.hs:200-261) */
 typedef struct { double x, y, z; } V3;
@@ -147,15 +163,15 @@ static V3 random_unit_vector(Rng* g) {
     double zz = D(g);
     double z = (zz * 2.0) - 1.0;
     double r = sqrt(1.0 - z * z);
-    return v3(r * cos(a), r * sin(a), z);
+    return v3(r * o_cos(a), r * o_sin(a), z);
 }
 /* randomCosineDirection (src/Lib.hs:1206-1217) */
 static V3 random_cosine_direction(Rng* g) {
     double r1 = D(g), r2 = D(g);
     double z = sqrt(1.0 - r2);
     double phi = 2.0 * PI * r1;
-    double x = cos(phi) * sqrt(r2);
-    double y = sin(phi) * sqrt(r2);
+    double x = o_cos(phi) * sqrt(r2);
+    double y = o_sin(phi) * sqrt(r2);
     return v3(x, y, z);
 }
 /* randomToSphereM (src/Lib.hs:1219-1228) */
@@ -164,7 +180,7 @@ static V3 random_to_sphere(Rng* g, double radius, double dist_squared) {
     double z = 1.0 + r2 * (sqrt(1.0 - radius * radius / dist_squared) - 1.0);
     double phi = 2.0 * PI * r1;
     double s = sqrt(1.0 - z * z);
-    return v3(cos(phi) * s, sin(phi) * s, z);
+    return v3(o_cos(phi) * s, o_sin(phi) * s, z);
 }
 
 /* ------------------------------------------------------------------ ONB (src/Lib.hs:263-279) */
@@ -185,9 +201,9 @@ static V3 onb_local_v(ONB o, V3 a) { /* scale a u |+| scale b v |+| scale c w */
 /* RealFloat class default (GHC.Float), used by `hit Sphere` (src/Lib.hs:1102). */
 static int is_neg_zero(double x) { return x == 0.0 && signbit(x); }
 double oracle_ghc_atan2(double y, double x) {
-    if (x > 0) return atan(y / x);
+    if (x > 0) return o_atan(y / x);
     if (x == 0 && y > 0) return PI / 2;
-    if (x < 0 && y > 0) return PI + atan(y / x);
+    if (x < 0 && y > 0) return PI + o_atan(y / x);
     if ((x <= 0 && y < 0) || (x < 0 && is_neg_zero(y)) || (is_neg_zero(x) && is_neg_zero(y)))
         return -oracle_ghc_atan2(-y, x);
     if (y == 0 && (x < 0 || is_neg_zero(x))) return PI;
@@ -257,10 +273,10 @@ static V3 texture_value(const Ctx* c, int tid, double u, double v, V3 p) {
     case RT_TEX_CONSTANT:
         return v3(t->f[0], t->f[1], t->f[2]);
     case RT_TEX_CHECKER:
-        if (sin(10 * p.x) * sin(10 * p.y) * sin(10 * p.z) < 0) return texture_value(c, t->a, u, v, p);
+        if (o_sin(10 * p.x) * o_sin(10 * p.y) * o_sin(10 * p.z) < 0) return texture_value(c, t->a, u, v, p);
         return texture_value(c, t->b, u, v, p);
     case RT_TEX_PERLIN: {
-        double m = 0.5 * (1.0 + sin(p.z + 10 * turb(&c->s->perlins[t->a], t->f[0], p, 7)));
+        double m = 0.5 * (1.0 + o_sin(p.z + 10 * turb(&c->s->perlins[t->a], t->f[0], p, 7)));
         return scale(m, v3(1.0, 1.0, 1.0));
     }
     case RT_TEX_IMAGE: {
@@ -338,7 +354,7 @@ static int sphere_hit(V3 sc, double sr, int sm, Ray r, double t_min, double t_ma
     V3 outward = divide(vsub(h->p, sc), sr);
     face_normal(r, outward, &h->ff, &h->n);
     double phi = oracle_ghc_atan2(outward.z, outward.x);
-    double theta = asin(outward.y);
+    double theta = o_asin(outward.y);
     h->u = 1.0 - ((phi + PI) / (2 * PI));
     h->v = (theta + (PI / 2)) / PI;
     h->mat = sm;
@@ -429,7 +445,7 @@ static int hit(const Ctx* c, int id, Ray r, double t_min, double t_max, Rng* g, 
         double ray_length = vlength(r.d);
         double dist_inside = (rec2t - rec1t) * ray_length;
         double rnd = D(g);
-        double hit_dist = n->f[0] * log(rnd);
+        double hit_dist = n->f[0] * o_log(rnd);
         if (hit_dist > dist_inside) return 0;
         double newt = rec1t + (hit_dist / ray_length);
         h->t = newt;
@@ -526,7 +542,7 @@ static V3 refract(V3 v, V3 n, double eta) {                                 /* L
 static double schlick(double cosine, double ref_idx) { /* Lib.hs:899-903 */
     double r0 = (1.0 - ref_idx) / (1.0 + ref_idx);
     double r1 = r0 * r0;
-    return r1 + (1.0 - r1) * pow(1 - cosine, 5);
+    return r1 + (1.0 - r1) * o_pow5(1 - cosine);
 }
 
 typedef struct { Ray ray; int specular; V3 att; double pdf; } Scatter;
@@ -720,7 +736,9 @@ int oracle_render_rows(const rt_scene_desc* scene, const rt_camera* cam, const r
     if (!scene || !cam || !p || p->width <= 0 || p->height <= 0 || p->spp <= 0) return -1;
     if (row0 < 0 || row1 > p->height || row0 > row1) return -1;
     if (p->rng_mode == RT_RNG_EXACT && (row0 != 0 || !col_gens)) return -1;
+    if ((p->flags & RT_FLAG_SHARED_LIBM) && p->rng_mode != RT_RNG_EXACT) return -1; /* (as rt_render) */
     const int W = p->width, H = p->height;
+    g_shared_libm = (p->flags & RT_FLAG_SHARED_LIBM) != 0;
     if (counters) memset(counters, 0, sizeof(int64_t) * C_NCOUNTERS);
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
@@ -775,7 +793,25 @@ int oracle_render_rows(const rt_scene_desc* scene, const rt_camera* cam, const r
             }
         }
     }
+    g_shared_libm = 0;
     return 0;
+}
+
+/* include/rt_libm.h on the host (tests compare the device's evaluation of the same functions):
+   op 12 sin, 13 cos, 14 atan, 15 asin, 16 log, 17 GHC atan2(x, y) over them (rt_debug_math's ids). */
+void oracle_shared_libm(int op, const double* x, const double* y, int n, double* out) {
+    g_shared_libm = 1;
+    for (int i = 0; i < n; ++i) {
+        switch (op) {
+            case 12: out[i] = rtlm_sin(x[i]); break;
+            case 13: out[i] = rtlm_cos(x[i]); break;
+            case 14: out[i] = rtlm_atan(x[i]); break;
+            case 15: out[i] = rtlm_asin(x[i]); break;
+            case 16: out[i] = rtlm_log(x[i]); break;
+            default: out[i] = oracle_ghc_atan2(x[i], y[i]); break;
+        }
+    }
+    g_shared_libm = 0;
 }
 
 int oracle_render(const rt_scene_desc* scene, const rt_camera* cam, const rt_render_params* p,

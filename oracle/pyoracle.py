@@ -51,6 +51,8 @@ def lib():
         L.oracle_num_counters.restype = C.c_int
         L.oracle_probe.restype = C.c_int
         L.oracle_probe.argtypes = [C.c_void_p, C.c_void_p, C.c_int, P(D), C.c_int, U64, P(D)]
+        L.oracle_shared_libm.restype = None
+        L.oracle_shared_libm.argtypes = [C.c_int, P(D), P(D), C.c_int, P(D)]
         _lib = L
     return _lib
 
@@ -127,3 +129,14 @@ def philox(ctr, key):
     o = (C.c_uint32 * 4)()
     lib().oracle_philox(c, k, o)
     return [int(x) for x in o]
+
+
+def shared_libm(op, x, y=None):
+    """include/rt_libm.h evaluated on the host (op ids as rt_debug_math: 12 sin ... 17 GHC atan2)."""
+    x = np.ascontiguousarray(x, dtype=np.float64).reshape(-1)
+    y = np.zeros_like(x) if y is None else np.ascontiguousarray(y, dtype=np.float64).reshape(-1)
+    out = np.zeros_like(x)
+    P = C.POINTER
+    lib().oracle_shared_libm(op, x.ctypes.data_as(P(C.c_double)), y.ctypes.data_as(P(C.c_double)), x.size,
+                             out.ctypes.data_as(P(C.c_double)))
+    return out

@@ -10,6 +10,7 @@
 
 #include "rt.h"
 #include "rt_layout.h"
+#include "rt_libm.h"
 #include "rt_wide.h"
 
 
@@ -45,6 +46,36 @@ struct Ray {
   V3 o, d;
   double tm;
 };
+
+// The transcendentals of the path: OCML, or (SL, tier A with RT_FLAG_SHARED_LIBM) the portable ones of
+// include/rt_libm.h that the oracle evaluates too, bit for bit.
+template <bool SL>
+__device__ __forceinline__ double m_sin(double x) {
+  if constexpr (SL) return rtlm_sin(x);
+  else return sin(x);
+}
+template <bool SL>
+__device__ __forceinline__ double m_cos(double x) {
+  if constexpr (SL) return rtlm_cos(x);
+  else return cos(x);
+}
+template <bool SL>
+__device__ __forceinline__ double m_log(double x) {
+  if constexpr (SL) return rtlm_log(x);
+  else return log(x);
+}
+template <bool SL>
+__device__ __forceinline__ double m_atan(double x) {
+  if constexpr (SL) return rtlm_atan(x);
+  else return atan(x);
+}
+template <bool SL>
+__device__ __forceinline__ double m_asin(double x) {
+  if constexpr (SL) return rtlm_asin(x);
+  else return asin(x);
+}
+template <unsigned F>
+constexpr bool kSL = (F & F_SLIBM) != 0;
 
 // Correctly rounded a / b from y = RN(1/b): two Markstein residual corrections (each residual
 // a - b*q is exact under FMA when nothing under- or overflows), then a range guard that falls back
@@ -152,8 +183,11 @@ __device__ __forceinline__ double word_to_draw(uint64_t w) {
   return 1.0 - (double)w / 18446744073709551616.0;
 }
 
-// Tier A: the reference's SplitMix64 stream (nextWord64).
-struct RngExact {
+// Tier A: the reference's SplitMix64 stream (nextWord64). SL: the draws' transcendentals (random unit
+// vectors, cosine directions, sphere samples, media distances) from rt_libm.h.
+template <bool SL = false>
+struct RngExactT {
+  static constexpr bool kSL = SL;
   uint64_t seed, gamma;
   __device__ __forceinline__ void reserve(int) {}
   __device__ __forceinline__ double draw() {
@@ -161,6 +195,7 @@ struct RngExact {
     return word_to_draw(mix64(seed));
   }
 };
+using RngExact = RngExactT<false>;
 
 // Tier B: Philox4x32-10, key = seed, counter = {pair, sample, pixel, 0}; two draws per block.
 __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
@@ -184,6 +219,7 @@ __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) 
 // the FIFO. (Blocks computed inside every divergent draw site would each cost the wave a full
 // Philox evaluation.) The sequence of words is the stream's, whatever the reserve points.
 struct RngPhilox {
+  static constexpr bool kSL = false;
   uint32_t k0, k1, pid, sample, pair;
   uint32_t n;  // buffered words
   uint64_t w0, w1, w2, w3;
@@ -272,7 +308,7 @@ __device__ __forceinline__ V3 random_unit_vector(R& g) {  // Lib.hs:1187-1197
   const double zz = g.draw();
   const double z = (zz * 2.0) - 1.0;
   const double r = sqrt(1.0 - z * z);
-  return v3(r * cos(a), r * sin(a), z);
+  return v3(r * m_cos<R::kSL>(a), r * m_sin<R::kSL>(a), z);
 }
 template <class R>
 __device__ __forceinline__ V3 random_cosine_direction(R& g) {  // Lib.hs:1206-1217
@@ -280,7 +316,7 @@ __device__ __forceinline__ V3 random_cosine_direction(R& g) {  // Lib.hs:1206-12
   const double z = sqrt(1.0 - r2);
   const double phi = 2.0 * kPi * r1;
   const double sr2 = sqrt(r2);
-  return v3(cos(phi) * sr2, sin(phi) * sr2, z);
+  return v3(m_cos<R::kSL>(phi) * sr2, m_sin<R::kSL>(phi) * sr2, z);
 }
 template <class R>
 __device__ __forceinline__ V3 random_to_sphere(R& g, double radius, double dist_squared) {  // Lib.hs:1219-1228
@@ -288,7 +324,7 @@ __device__ __forceinline__ V3 random_to_sphere(R& g, double radius, double dist_
   const double z = 1.0 + r2 * (sqrt(1.0 - radius * radius / dist_squared) - 1.0);
   const double phi = 2.0 * kPi * r1;
   const double s = sqrt(1.0 - z * z);
-  return v3(cos(phi) * s, sin(phi) * s, z);
+  return v3(m_cos<R::kSL>(phi) * s, m_sin<R::kSL>(phi) * s, z);
 }
 
 // ------------------------------------------------------------------ ONB (Lib.hs:263-279)
@@ -309,6 +345,7 @@ __device__ __forceinline__ V3 onb_local(const ONB& o, V3 a) {
 
 // GHC's RealFloat-default atan2 (GHC.Float), used by `hit Sphere` for u (Lib.hs:1102).
 __device__ __forceinline__ bool neg_zero(double x) { return x == 0.0 && signbit(x); }
+template <bool SL = false>
 __device__ inline double ghc_atan2(double y, double x) {
   double sgn = 1.0;
   // -atan2 (-y) x branch, applied at most once (it maps y < 0 to y > 0 / y = +0)
@@ -317,9 +354,9 @@ __device__ inline double ghc_atan2(double y, double x) {
     y = -y;
   }
   double r;
-  if (x > 0) r = atan(y / x);
+  if (x > 0) r = m_atan<SL>(y / x);
   else if (x == 0 && y > 0) r = kPi / 2;
-  else if (x < 0 && y > 0) r = kPi + atan(y / x);
+  else if (x < 0 && y > 0) r = kPi + m_atan<SL>(y / x);
   else if (y == 0 && (x < 0 || neg_zero(x))) r = kPi;
   else if (x == 0 && y == 0) r = y;
   else r = x + y;

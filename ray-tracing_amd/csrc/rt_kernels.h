@@ -649,7 +649,7 @@ __global__ void __launch_bounds__(RT_BLOCK) render_exact(RenderArgs A) {
   S.world = S.world_ref;
   const int x = blockIdx.x * RT_BLOCK + threadIdx.x;
   if (x >= A.W) return;
-  RngExact g{A.gens[2 * x], A.gens[2 * x + 1]};
+  RngExactT<kSL<F>> g{A.gens[2 * x], A.gens[2 * x + 1]};
   const int ns = A.spp;
   for (int row = 0; row < A.H; ++row) {
     const int y = A.H - 1 - row;
@@ -814,6 +814,13 @@ __global__ void math_probe(int op, const double* x, const double* y, int n, doub
     case 8: r = pow(a, b); break;
     case 9: r = ghc_atan2(a, b); break;
     case 11: r = pow5(a); break;
+    // the shared portable functions (include/rt_libm.h; RT_FLAG_SHARED_LIBM)
+    case 12: r = rtlm_sin(a); break;
+    case 13: r = rtlm_cos(a); break;
+    case 14: r = rtlm_atan(a); break;
+    case 15: r = rtlm_asin(a); break;
+    case 16: r = rtlm_log(a); break;
+    case 17: r = ghc_atan2<true>(a, b); break;
     default: r = tan(a); break;
   }
   out[i] = r;

@@ -51,8 +51,10 @@ enum : unsigned {
   F_UV = 64u,     // always compute sphere (u, v) (debug queries)
   F_COUNT = 128u, // counting build: per-lane work counters (DESIGN.md "Roofline")
   F_WIDE = 256u,  // resumable walk over the 4-wide fp32-box tree (rt_wide.h) instead of the binary one
-  F_MIXW = 1024u  // the mixed walk (media / frame worlds) enters 4-wide fp32-box trees built over the
+  F_MIXW = 1024u, // the mixed walk (media / frame worlds) enters 4-wide fp32-box trees built over the
                   // re-bounded subtrees (RT_WROOT nodes) instead of walking them node by node
+  F_SLIBM = 2048u // tier A with RT_FLAG_SHARED_LIBM: sin / cos / log / atan / asin from include/rt_libm.h
+                  // (the oracle's too) instead of OCML
 };
 
 // Kernel variants: spheres-only (configs 1, 2, 5), Cornell-like (rects, instances, lights), full.

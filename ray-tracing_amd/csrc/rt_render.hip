@@ -175,6 +175,8 @@ int check_params(const rt_render_params* p) {
   if (p->width <= 0 || p->height <= 0 || p->spp <= 0 || p->max_depth < 0)
     return invalid("width/height/spp must be positive and max_depth >= 0");
   if (p->rng_mode != RT_RNG_EXACT && p->rng_mode != RT_RNG_PHILOX) return invalid("unknown rng_mode");
+  if ((p->flags & RT_FLAG_SHARED_LIBM) && p->rng_mode != RT_RNG_EXACT)
+    return invalid("RT_FLAG_SHARED_LIBM is a tier-A (RT_RNG_EXACT) flag");
   const int tile = p->tile ? p->tile : 16;
   if (tile <= 0 || tile % 8 || tile > 256) return invalid("tile must be a multiple of 8 in [8, 256]");
   if (p->shard_count < 0 || (p->shard_count > 0 && (p->shard_rank < 0 || p->shard_rank >= p->shard_count)) ||
@@ -220,11 +222,13 @@ bool env_off(const char* name) {
   const char* e = std::getenv(name);
   return e && e[0] == '0';
 }
-const void* exact_variant(unsigned f) {
+const void* exact_variant(unsigned f, bool shared_libm) {
   switch (variant_for(f)) {
-    case kVarSpheres: return (const void*)render_exact<kVarSpheres>;
-    case kVarCornell: return (const void*)render_exact<kVarCornell>;
-    default: return (const void*)render_exact<F_ALL>;
+    case kVarSpheres:
+      return shared_libm ? (const void*)render_exact<kVarSpheres | F_SLIBM> : (const void*)render_exact<kVarSpheres>;
+    case kVarCornell:
+      return shared_libm ? (const void*)render_exact<kVarCornell | F_SLIBM> : (const void*)render_exact<kVarCornell>;
+    default: return shared_libm ? (const void*)render_exact<F_ALL | F_SLIBM> : (const void*)render_exact<F_ALL>;
   }
 }
 
@@ -872,7 +876,7 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, cons
     A.out_lin = d_img_lin;
     HIPCHK(hipEventRecord(c->ev0, st));
     void* args[] = {&A};
-    HIPCHK(hipLaunchKernel(exact_variant(c->features), dim3((p.width + RT_BLOCK - 1) / RT_BLOCK), dim3(RT_BLOCK),
+    HIPCHK(hipLaunchKernel(exact_variant(c->features, (p.flags & RT_FLAG_SHARED_LIBM) != 0), dim3((p.width + RT_BLOCK - 1) / RT_BLOCK), dim3(RT_BLOCK),
                            args, 0, st));
     HIPCHK(hipEventRecord(c->ev1, st));
     if (out_gens)
@@ -1020,7 +1024,7 @@ int rt_debug_probe(rt_ctx* c, const rt_camera* cam, int op, const double* in, in
 }
 
 int rt_debug_math(rt_ctx* c, int op, const double* x, const double* y, int n, double* out) {
-  if (!c || !x || !y || !out || n < 0 || op < 0 || op > 11) return invalid("rt_debug_math: bad argument");
+  if (!c || !x || !y || !out || n < 0 || op < 0 || op > 17) return invalid("rt_debug_math: bad argument");
   if (n == 0) return RT_OK;
   DEVICE_SCOPE(c->device);
   const size_t bytes = sizeof(double) * (size_t)n;

@@ -60,8 +60,9 @@ __device__ inline double turb(const rt_perlin* P, double sc, V3 p) {  // Lib.hs:
 // marbleTexture's value (Lib.hs:505-507). Not inlined, like sphere_uv: inlined into a render loop, the
 // turbulence's 56 unrolled lattice corners and sin's coefficients raise the whole loop's register
 // pressure (the full variant: 352 -> ~290 B/lane of scratch); as a call it costs only Perlin hits.
+template <bool SL>
 __device__ __noinline__ double marble(const rt_perlin* P, double sc, V3 p) {
-  return 0.5 * (1.0 + sin(p.z + 10 * turb(P, sc, p)));
+  return 0.5 * (1.0 + m_sin<SL>(p.z + 10 * turb(P, sc, p)));
 }
 // textureValue (Lib.hs:496-510); checker chains are followed iteratively.
 template <unsigned F>
@@ -69,11 +70,11 @@ __device__ inline V3 texture_value(const Scene& S, int tid, double u, double v, 
   const rt_texture* t = &S.texs[tid];
   if constexpr (!(F & F_TEX)) return v3(t->f[0], t->f[1], t->f[2]);
   while (t->type == RT_TEX_CHECKER) {
-    const bool odd = sin(10 * p.x) * sin(10 * p.y) * sin(10 * p.z) < 0;
+    const bool odd = m_sin<kSL<F>>(10 * p.x) * m_sin<kSL<F>>(10 * p.y) * m_sin<kSL<F>>(10 * p.z) < 0;
     t = &S.texs[odd ? t->a : t->b];
   }
   if (t->type == RT_TEX_CONSTANT) return v3(t->f[0], t->f[1], t->f[2]);
-  if (t->type == RT_TEX_PERLIN) return scale(marble(&S.perlins[t->a], t->f[0], p), v3(1.0, 1.0, 1.0));
+  if (t->type == RT_TEX_PERLIN) return scale(marble<kSL<F>>(&S.perlins[t->a], t->f[0], p), v3(1.0, 1.0, 1.0));
   // RT_TEX_IMAGE
   if (t->a < 0) return v3(0, 1, 1);
   const rt_image im = S.images[t->a];
@@ -227,9 +228,10 @@ __device__ __noinline__ double log_call(double x) { return log(x); }
 // asin bring polynomial coefficients that, inlined into a render loop, the compiler materialises once
 // for the whole loop and spills (the full variant: 560 -> ~290 B/lane of scratch); as a call they are
 // materialised per call, and only image-textured hits make it.
+template <bool SL>
 __device__ __noinline__ void sphere_uv(V3 outward, double& u, double& v) {
-  const double phi = ghc_atan2(outward.z, outward.x);
-  const double theta = asin(outward.y);
+  const double phi = ghc_atan2<SL>(outward.z, outward.x);
+  const double theta = m_asin<SL>(outward.y);
   u = 1.0 - ((phi + kPi) / (2 * kPi));
   v = (theta + (kPi / 2)) / kPi;
 }
@@ -244,7 +246,7 @@ __device__ __forceinline__ void sphere_record(const Scene& S, V3 sc, double sr, 
   face_normal(r, outward, h.ff, h.n);
   h.mat = sm;
   if ((F & F_UV) || ((F & F_TEX) && S.mats[sm].needs_uv)) {  // u, v only feed image textures
-    sphere_uv(outward, h.u, h.v);
+    sphere_uv<kSL<F>>(outward, h.u, h.v);
   } else {
     h.u = 0.0;
     h.v = 0.0;
@@ -424,7 +426,7 @@ __device__ inline bool medium_hit(const Scene& S, const rt_node* n, const RayX& 
   const double ray_length = vlen(r.d);
   const double dist_inside = (rec2t - rec1t) * ray_length;
   const double rnd = g.draw();
-  const double hit_dist = n->f[0] * log(rnd);
+  const double hit_dist = n->f[0] * m_log<R::kSL>(rnd);
   if (hit_dist > dist_inside) return false;
   const double newt = rec1t + (hit_dist / ray_length);
   h.t = newt;
@@ -1387,21 +1389,9 @@ __device__ __forceinline__ V3 refract(V3 v, V3 n, double eta) {
 // is the correctly rounded x^5 (glibc's pow is within 0.52 ulp of it; OCML's pow(x, 5) matched
 // glibc in 76 % of cases). No polynomial constants either: the compiler hoisted OCML pow's into
 // registers for the whole kernel and spilled them. Zeros, NaN, infinities and magnitudes outside
-// [2^-200, 2^200] (x = 1 - cos theta lies in [0, 2]) take the plain product.
-__device__ __forceinline__ double pow5(double x) {
-  const double ax = fabs(x);
-  if (!(ax >= 0x1p-200 && ax <= 0x1p200)) return x * x * x * x * x;
-  const double h2 = x * x, l2 = fma(x, x, -h2);
-  double h4 = h2 * h2, l4 = fma(h2, h2, -h4);
-  l4 = fma(2.0 * h2, l2, l4);  // (h2 + l2)^2 = h2^2 + 2 h2 l2 (+ l2^2, below 2^-104 relative)
-  const double s4 = h4 + l4;
-  l4 = l4 - (s4 - h4);
-  h4 = s4;
-  const double h5 = h4 * x;
-  double l5 = fma(h4, x, -h5);
-  l5 = fma(l4, x, l5);
-  return h5 + l5;
-}
+// [2^-200, 2^200] (x = 1 - cos theta lies in [0, 2]) take the plain product. (Shared with the oracle's
+// RT_FLAG_SHARED_LIBM mode: include/rt_libm.h.)
+__device__ __forceinline__ double pow5(double x) { return rtlm_pow5(x); }
 __device__ __forceinline__ double schlick(double cosine, double ref_idx) {
   const double r0 = (1.0 - ref_idx) / (1.0 + ref_idx);
   const double r1 = r0 * r0;

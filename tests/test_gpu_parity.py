@@ -109,17 +109,46 @@ def test_tier_a_rng_consuming_features(gpu_ctx, name, camname, w, h, spp):
     """Tier A (RT_RNG_EXACT, the drop-in runRenderAMD's mode: the reference's per-column SplitMix streams)
     against the oracle on every feature that consumes draws: medium draws interleaved with the walk
     (Lib.hs:1053-1080), the motion-blur time draw (Lib.hs:1253-1267, 1106-1108), Isotropic's rejection
-    draws (Lib.hs:861-865), Perlin and image textures. The end-of-stream generators count every column's
-    draws: they must be equal."""
+    draws (Lib.hs:861-865), Perlin and image textures.
+    1. RT_FLAG_SHARED_LIBM (both sides evaluate sin/cos/log/atan/asin in include/rt_libm.h): bytes, linear
+       averages and end-of-stream generators bit-identical on every scene.
+    2. Each side's own libm (OCML on the device, glibc in the oracle): the north-star tolerance and equal
+       end generators, except where a column's serial stream meets a libm ulp that later flips a branch
+       (next_week_final: thousands of fog bounces per column). There the columns that consumed the same
+       draws (equal end generators) must match to the tolerance, and the oracle with glibc against the
+       oracle with rt_libm.h diverges in the same way: a libm property, not a device one."""
     earth = np.load(_earth_path())["rgb"] if name in ("earth", "random", "next_week_final") else None
     sc, g1 = _scene(name, earth=earth)
     cam = rtamd.camera(camname, w, h)
     gens = rtamd.column_gens(g1, w)
+    gpu_ctx.upload(sc)
+    p = rtamd.make_params(w, h, spp, 50, rtamd.RT_RNG_EXACT, flags=rtamd.RT_FLAG_SHARED_LIBM)
+    rgb_g, lin_g, gens_g = gpu_ctx.render(cam, p, gens, linear=True, want_gens=True)
+    rgb_o, lin_o, gens_o, _ = pyoracle.render(sc, cam, p, col_gens=gens)
+    print(f"{name} tier A, shared libm: bytes equal {float((rgb_g == rgb_o).mean()):.6f}, linear bit-identical "
+          f"{float(((lin_g == lin_o) | (np.isnan(lin_g) & np.isnan(lin_o))).mean()):.6f}, end generators equal "
+          f"{float((gens_g == gens_o).all(axis=1).mean()):.6f}")
+    assert np.array_equal(gens_g, gens_o) and np.array_equal(rgb_g, rgb_o)
+    assert np.array_equal(lin_g, lin_o, equal_nan=True)
     p = rtamd.make_params(w, h, spp, 50, rtamd.RT_RNG_EXACT)
-    _, _, gens_g, gens_o = _cmp(gpu_ctx, sc, cam, p, col_gens=gens, what=f"{name} tier A")
-    eq = (gens_g == gens_o).all(axis=1).mean()
-    print(f"{name} tier A: end generators equal in {eq:.6f} of columns")
-    assert np.array_equal(gens_g, gens_o)
+    rgb_g, lin_g, gens_g = gpu_ctx.render(cam, p, gens, linear=True, want_gens=True)
+    rgb_o, lin_o, gens_o, _ = pyoracle.render(sc, cam, p, col_gens=gens)
+    ok, eq, dmax = parity(lin_g, lin_o, rgb_g, rgb_o)
+    same_cols = (gens_g == gens_o).all(axis=1)
+    print(f"{name} tier A, device libm vs glibc: channels within 1e-3 {ok:.6f}, bytes equal {eq:.6f}, max |d| "
+          f"{dmax:.3g}, end generators equal in {same_cols.mean():.6f} of columns")
+    if name != "next_week_final":
+        assert ok >= 0.999 and eq >= 0.999 and same_cols.all()
+        return
+    ok_c, eq_c, _ = parity(lin_g[:, same_cols], lin_o[:, same_cols], rgb_g[:, same_cols], rgb_o[:, same_cols])
+    ps = rtamd.make_params(w, h, spp, 50, rtamd.RT_RNG_EXACT, flags=rtamd.RT_FLAG_SHARED_LIBM)
+    rgb_s, lin_s, gens_s, _ = pyoracle.render(sc, cam, ps, col_gens=gens)
+    ok_l, eq_l, _ = parity(lin_s, lin_o, rgb_s, rgb_o)
+    print(f"  columns with equal end generators: channels within 1e-3 {ok_c:.6f}, bytes equal {eq_c:.6f}; oracle "
+          f"glibc vs rt_libm.h: channels within 1e-3 {ok_l:.6f}, end generators equal in "
+          f"{(gens_s == gens_o).all(axis=1).mean():.6f} of columns")
+    assert same_cols.mean() >= 0.5 and ok_c >= 0.999 and eq_c >= 0.999
+    assert (gens_s == gens_o).all(axis=1).mean() < 1.0  # (the libm swap alone diverges columns too)
 
 
 @pytest.mark.parametrize("name,camname", [("cornell_smoke", "cornell"), ("simple_light", "two_spheres"),
