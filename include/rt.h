@@ -502,6 +502,17 @@ int rt_debug_closest_hits(rt_ctx* ctx, const double* rays, int n, double tmin, d
  *   RT_PROBE_TEXTURE      textureValue (src/Lib.hs:496-513): texture id, u, v, p3 -> albedo3
  *   RT_PROBE_GET_RAY      getRay with `cam` (src/Lib.hs:1253-1267): s, t -> ray o3 d3 tm, words
  */
+/*
+ * Debug / parity entry: tier A (RT_RNG_EXACT) over the whole frame, with column `col`'s path segments
+ * recorded: 10 doubles per segment {row, sample (in the order rendered), seg (or -(seg + 1) where the
+ * path ends), the scattered ray's origin xyz and direction xyz (at the end: the segment's own ray), the
+ * column generator's seed after the segment (the uint64 bits)}. *out_n = segments recorded (at most
+ * cap). The oracle's oracle_exact_trace records the same, so the first differing record localises a
+ * tier-A divergence.
+ */
+int rt_debug_exact_trace(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* p, const uint64_t* col_gens,
+                         int col, double* out, int cap, int* out_n);
+
 #define RT_PROBE_SCATTER 0
 #define RT_PROBE_HTBL_RANDOM 1
 #define RT_PROBE_HTBL_PDF 2

@@ -10,9 +10,11 @@
 --
 -- UNTESTED AS HASKELL: no GHC exists in the build image or on the GPU box (SURVEY.md §0.2), so this
 -- file has never been compiled. Its call sequence — post-order flattening of the Hittable tree into
--- an rt_scene_desc, rt_create, rt_upload_scene, rt_render (tier A, one SplitMix generator per
--- column), rows split top first, rt_destroy — is mirrored in C by tests/c/ffi_sequence.c, which
--- tests/test_ffi_sequence.py compiles and runs (the rendering half on the GPU).
+-- an rt_scene_desc, rt_create_multi over every visible GPU (rt_device_count), rt_upload_scene,
+-- rt_render (tier A, one SplitMix generator per column; tier B tile-sharded over the GPUs and gathered
+-- with RCCL inside librtamd), rows split top first, rt_destroy — is mirrored in C by
+-- tests/c/ffi_sequence.c, which tests/test_ffi_sequence.py compiles and runs (the rendering half on the
+-- GPU, checked against the CPU oracle on the same flattened records).
 --
 -- What the reference package needs for it (integration/reference.patch, a `patch -p1` against the
 -- reference's root; then copy this file to src/RenderAMD.hs):
@@ -66,8 +68,11 @@ data SceneDesc     -- rt_scene_desc, 112 bytes
 data CameraRec     -- rt_camera, 192 bytes
 data RenderParams  -- rt_render_params, 48 bytes
 
-foreign import ccall unsafe "rt.h rt_create"
-  c_rt_create :: CInt -> Ptr (Ptr RtCtx) -> IO CInt
+foreign import ccall unsafe "rt.h rt_device_count"
+  c_rt_device_count :: Ptr CInt -> IO CInt
+-- one ctx over n GPUs (NULL device list = 0..n-1): tier-B frames shard over them, RCCL gathers
+foreign import ccall unsafe "rt.h rt_create_multi"
+  c_rt_create_multi :: CInt -> Ptr CInt -> Ptr (Ptr RtCtx) -> IO CInt
 foreign import ccall unsafe "rt.h rt_destroy"
   c_rt_destroy :: Ptr RtCtx -> IO ()
 foreign import ccall safe "rt.h rt_upload_scene"
@@ -377,7 +382,8 @@ withParams w h ns maxDepth rng seed k =
 columnGens :: [RandGen] -> [Word64]
 columnGens gens = concat [[s, g] | RandGen std <- gens, let (s, g) = unseedSMGen (unStdGen std)]
 
--- | Render on device 0; the raw H x W x 3 bytes, top row first.
+-- | Render on every visible GPU (tier B: tile shards gathered by RCCL; tier A: per-column streams do not
+-- shard, the first GPU renders); the raw H x W x 3 bytes, top row first.
 renderBytes :: Scene -> Camera -> (Int, Int) -> Int -> Int -> Int32 -> Word64 -> [Word64]
             -> IO (SV.Vector Word8)
 renderBytes scene cam (w, h) ns maxDepth rng seed gensW = do
@@ -392,8 +398,10 @@ renderBytes scene cam (w, h) ns maxDepth rng seed gensW = do
         check "rt_render" (c_rt_render ctx pc pp (if rng == rtRngExact then pg else nullPtr) po nullPtr nullPtr)
     SV.unsafeFreeze out
   where
-    acquire = alloca $ \pctx -> do
-      check "rt_create" (c_rt_create 0 pctx)
+    acquire = alloca $ \pn -> alloca $ \pctx -> do
+      check "rt_device_count" (c_rt_device_count pn)
+      n <- peek pn
+      check "rt_create_multi" (c_rt_create_multi (min n 16) nullPtr pctx)  -- (RT_MAX_DEVICES = 16)
       peek pctx
 
 -- | Rows of pixels, top row first, each `cols` wide.

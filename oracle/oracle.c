@@ -621,16 +621,31 @@ static V3 emitted(const Ctx* c, const rt_material* m, const Hit* h) {
     return v3(0, 0, 0);
 }
 
+/* Tier-A path trace of one column (oracle_exact_trace; NULL otherwise): 10 doubles per segment. */
+static double* g_tr = NULL;
+static int g_tr_n = 0, g_tr_cap = 0, g_tr_row = 0, g_tr_j = 0;
+static void trace_seg(int seg, int end, Ray r, const Rng* g) {
+    if (!g_tr || g_tr_n >= g_tr_cap) return;
+    double* o = g_tr + 10 * (size_t)g_tr_n++;
+    o[0] = g_tr_row; o[1] = g_tr_j; o[2] = end ? -(seg + 1) : seg;
+    o[3] = r.o.x; o[4] = r.o.y; o[5] = r.o.z; o[6] = r.d.x; o[7] = r.d.y; o[8] = r.d.z;
+    memcpy(&o[9], &g->seed, 8);
+}
+
 /* rayColor (src/Lib.hs:1297-1333), recursion in the continuation's evaluation order:
  * specular: att |*| new; else att |*| (scatteringPdf `scale` (new `divide` pdfVal)). */
 static V3 ray_color(const Ctx* c, Ray r, int d, Rng* g) {
-    if (d <= 0) return v3(0, 0, 0);
+    if (d <= 0) { trace_seg(c->max_depth - d, 1, r, g); return v3(0, 0, 0); }
     CNT(c, C_WORLD_QUERIES);
     Hit h;
-    if (!hit(c, c->s->world_root, r, EPSILON, INFINITY, g, &h)) return vload(c->s->background);
+    if (!hit(c, c->s->world_root, r, EPSILON, INFINITY, g, &h)) {
+        trace_seg(c->max_depth - d, 1, r, g);
+        return vload(c->s->background);
+    }
     const rt_material* m = &c->s->materials[h.mat];
     Scatter s;
-    if (!scatter(c, m, r, &h, g, &s)) return emitted(c, m, &h);
+    if (!scatter(c, m, r, &h, g, &s)) { trace_seg(c->max_depth - d, 1, r, g); return emitted(c, m, &h); }
+    trace_seg(c->max_depth - d, 0, s.ray, g);
     V3 nw = ray_color(c, s.ray, d - 1, g);
     if (s.specular) return vmul(s.att, nw);
     double spdf = scattering_pdf(&h, s.ray);
@@ -673,6 +688,7 @@ static V3 render_pixel_exact(const Ctx* c, int x, int y, Rng* g, double* uvbuf) 
     }
     V3 acc = v3(0, 0, 0);
     for (int i = ns - 1; i >= 0; --i) {
+        g_tr_j = ns - 1 - i;
         Ray r = get_ray(c, uvbuf[2 * i], uvbuf[2 * i + 1], g);
         V3 c1 = ray_color(c, r, c->max_depth, g);
         acc = vadd(acc, c1);
@@ -794,6 +810,33 @@ int oracle_render_rows(const rt_scene_desc* scene, const rt_camera* cam, const r
         }
     }
     g_shared_libm = 0;
+    return 0;
+}
+
+/* Tier A, one column `col` of the frame, serially, with every path segment recorded: 10 doubles per
+   segment {row, sample, seg (or -(seg + 1) where the path ends), ray o xyz, d xyz (the scattered ray; at
+   the end the segment's own ray), the generator's seed after the segment (uint64 bits)}. The device's
+   rt_debug_exact_trace records the same: the first differing record localises a tier-A divergence. */
+int oracle_exact_trace(const rt_scene_desc* scene, const rt_camera* cam, const rt_render_params* p,
+                       const uint64_t* col_gens, int col, double* out, int cap, int* out_n) {
+    if (!scene || !cam || !p || !col_gens || col < 0 || col >= p->width || !out || cap < 0) return -1;
+    g_shared_libm = (p->flags & RT_FLAG_SHARED_LIBM) != 0;
+    Ctx c = {scene, cam, p->width, p->height, p->spp, p->max_depth, NULL};
+    double* uvbuf = (double*)malloc(sizeof(double) * 2 * (size_t)p->spp);
+    Rng g;
+    memset(&g, 0, sizeof g);
+    g.mode = RT_RNG_EXACT;
+    g.seed = col_gens[2 * col];
+    g.gamma = col_gens[2 * col + 1];
+    g_tr = out; g_tr_n = 0; g_tr_cap = cap;
+    for (int row = 0; row < p->height; ++row) {
+        g_tr_row = row;
+        (void)render_pixel_exact(&c, col, p->height - 1 - row, &g, uvbuf);
+    }
+    *out_n = g_tr_n;
+    g_tr = NULL;
+    g_shared_libm = 0;
+    free(uvbuf);
     return 0;
 }
 

@@ -51,6 +51,9 @@ def lib():
         L.oracle_num_counters.restype = C.c_int
         L.oracle_probe.restype = C.c_int
         L.oracle_probe.argtypes = [C.c_void_p, C.c_void_p, C.c_int, P(D), C.c_int, U64, P(D)]
+        L.oracle_exact_trace.restype = C.c_int
+        L.oracle_exact_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, P(U64), C.c_int, P(D), C.c_int,
+                                         P(C.c_int)]
         L.oracle_shared_libm.restype = None
         L.oracle_shared_libm.argtypes = [C.c_int, P(D), P(D), C.c_int, P(D)]
         _lib = L
@@ -140,3 +143,18 @@ def shared_libm(op, x, y=None):
     lib().oracle_shared_libm(op, x.ctypes.data_as(P(C.c_double)), y.ctypes.data_as(P(C.c_double)), x.size,
                              out.ctypes.data_as(P(C.c_double)))
     return out
+
+
+def exact_trace(scene, cam, params, col_gens, col, cap=1 << 20):
+    """oracle_exact_trace: tier A, column `col`, every path segment (10 doubles: row, sample, seg, o, d,
+    seed bits) — to compare with the device's rt_debug_exact_trace."""
+    gi = np.ascontiguousarray(col_gens, dtype=np.uint64).reshape(-1)
+    out = np.zeros((cap, 10), dtype=np.float64)
+    n = C.c_int(0)
+    P = C.POINTER
+    rc = lib().oracle_exact_trace(C.addressof(scene.desc), C.addressof(cam), C.addressof(params),
+                                  gi.ctypes.data_as(P(C.c_uint64)), col, out.ctypes.data_as(P(C.c_double)), cap,
+                                  C.byref(n))
+    if rc != 0:
+        raise RuntimeError(f"oracle_exact_trace failed ({rc})")
+    return out[: n.value].copy()

@@ -75,6 +75,9 @@ struct RenderArgs {
   uint64_t* gens;  // tier A: per-column (seed, gamma), updated in place
   int med_batch;   // binary walk of media worlds: lanes at a medium wait until this many are there (or
                    // nothing else walks); 0: never wait
+  double* trace;   // tier A, rt_debug_exact_trace: column trace_col's path segments (10 doubles each)
+  int* trace_n;
+  int trace_col, trace_cap;
 };
 
 // Slab pixel index -> image pixel (tile-major, 8x8 blocks inside a tile). Slab indices are < 2^32
@@ -407,7 +410,9 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
       ++cnt.oslot;
     }
     // ---- shade finished walks, then set up the next walk for every lane that is not walking
-    if (ready && t.tie && !t.redo) {  // exact tie: redo this walk as the reference does (once)
+    // exact tie, or a NaN-t rect hit in a re-bounded subtree (trav_take: `lite` in a first walk): redo
+    // this walk as the reference does (once)
+    if (ready && (t.tie || t.lite) && !t.redo) {
       ready = false;
       if constexpr ((F & F_COUNT) != 0) ++cnt.ties;
       trav_redo<F>(t, S.world_ref, INFINITY, g, walk_mark);
@@ -650,6 +655,8 @@ __global__ void __launch_bounds__(RT_BLOCK) render_exact(RenderArgs A) {
   const int x = blockIdx.x * RT_BLOCK + threadIdx.x;
   if (x >= A.W) return;
   RngExactT<kSL<F>> g{A.gens[2 * x], A.gens[2 * x + 1]};
+  const bool traced = A.trace && x == A.trace_col;
+  int tn = 0;
   const int ns = A.spp;
   for (int row = 0; row < A.H; ++row) {
     const int y = A.H - 1 - row;
@@ -666,13 +673,22 @@ __global__ void __launch_bounds__(RT_BLOCK) render_exact(RenderArgs A) {
       V3 thr = v3(1.0, 1.0, 1.0), contrib;
       int depth = A.max_depth;
       Cnt cnt{};
-      while (!segment<F>(A, S, ray, thr, depth, g, stk, contrib, cnt)) {
+      for (int seg = 0;; ++seg) {
+        const bool end = segment<F>(A, S, ray, thr, depth, g, stk, contrib, cnt);
+        if (traced && tn < A.trace_cap) {  // (rt_debug_exact_trace: the oracle's oracle_exact_trace layout)
+          double* o = A.trace + 10 * (long long)tn++;
+          o[0] = row, o[1] = j, o[2] = end ? -(seg + 1) : seg;
+          o[3] = ray.o.x, o[4] = ray.o.y, o[5] = ray.o.z, o[6] = ray.d.x, o[7] = ray.d.y, o[8] = ray.d.z;
+          o[9] = __longlong_as_double((long long)g.seed);
+        }
+        if (end) break;
       }
       sum = sum + contrib;
     }
     store_pixel(A, (long long)row * A.W + x, divide(sum, (double)ns));
   }
   A.gens[2 * x] = g.seed;
+  if (traced) *A.trace_n = tn;
 }
 
 // ---------------------------------------------------------------- slab -> image
@@ -719,7 +735,7 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
     if (S.ref_walk) trav_restart_ref(t, S.world, tmax);  // (the re-bounded skeleton, mixed walk)
     bool walking = true;
     walk_until<F>(S, t, walking, tmin, stk, RT_BLOCK, joint != 0, 0, 0, cnt, g, side);
-    if (t.tie) {
+    if (t.tie || t.lite) {
       trav_redo<F>(t, S.world_ref, tmax, g, 0u);
       while (trav_step<F>(S, t, tmin, stk, RT_BLOCK, joint != 0, cnt, g, side)) {
       }

@@ -871,6 +871,7 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, cons
     A.H = p.height;
     A.spp = p.spp;
     A.max_depth = p.max_depth;
+    A.flags = p.flags;  // (RT_FLAG_REFERENCE_CULL)
     A.gens = d_gens;
     A.out_rgb = d_img;
     A.out_lin = d_img_lin;
@@ -985,6 +986,53 @@ int rt_debug_closest_hits(rt_ctx* c, const double* rays, int n, double tmin, dou
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipMemcpy(out, d_out, sizeof(double) * 12 * (size_t)n, hipMemcpyDeviceToHost));
+  return RT_OK;
+}
+
+int rt_debug_exact_trace(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, const uint64_t* col_gens,
+                         int col, double* out, int cap, int* out_n) {
+  if (!c || !cam || !pin || !col_gens || !out || !out_n || cap < 0) return invalid("rt_debug_exact_trace: null argument");
+  rt_render_params p = *pin;
+  p.shard_rank = 0;
+  p.shard_count = 1;
+  int rc = check_params(&p);
+  if (rc) return rc;
+  if (p.rng_mode != RT_RNG_EXACT) return invalid("rt_debug_exact_trace: tier A only");
+  if (col < 0 || col >= p.width) return invalid("rt_debug_exact_trace: column out of range");
+  if (!c->has_scene) {
+    rt::set_error("rt_debug_exact_trace: no scene uploaded");
+    return RT_E_STATE;
+  }
+  DEVICE_SCOPE(c->device);
+  const long long npx = (long long)p.width * p.height;
+  DevBuf img, gens, tr, trn;
+  HIPCHK(hipMalloc(&img.p, (size_t)npx * 3));
+  HIPCHK(hipMalloc(&gens.p, sizeof(uint64_t) * 2 * (size_t)p.width));
+  HIPCHK(hipMalloc(&tr.p, sizeof(double) * 10 * (size_t)std::max(1, cap)));
+  HIPCHK(hipMalloc(&trn.p, sizeof(int)));
+  HIPCHK(hipMemcpy(gens.p, col_gens, sizeof(uint64_t) * 2 * (size_t)p.width, hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(trn.p, 0, sizeof(int)));
+  RenderArgs A{};
+  A.S = c->scene;
+  A.cam = *cam;
+  A.W = p.width;
+  A.H = p.height;
+  A.spp = p.spp;
+  A.max_depth = p.max_depth;
+  A.flags = p.flags;
+  A.gens = (uint64_t*)gens.p;
+  A.out_rgb = (uint8_t*)img.p;
+  A.trace = (double*)tr.p;
+  A.trace_n = (int*)trn.p;
+  A.trace_col = col;
+  A.trace_cap = cap;
+  void* args[] = {&A};
+  HIPCHK(hipLaunchKernel(exact_variant(c->features, (p.flags & RT_FLAG_SHARED_LIBM) != 0),
+                         dim3((p.width + RT_BLOCK - 1) / RT_BLOCK), dim3(RT_BLOCK), args, 0, c->stream));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpy(out_n, trn.p, sizeof(int), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(out, tr.p, sizeof(double) * 10 * (size_t)std::min(*out_n, cap), hipMemcpyDeviceToHost));
   return RT_OK;
 }
 

@@ -153,6 +153,10 @@ __device__ __forceinline__ bool box_hit(const double* f, const RayX& r, double t
   }
   const double band = 0x1p-48 * (fabs(L) + fabs(U));
   const bool ok_band = (band > 0x1p-1000) & (band < INFINITY);  // (L and U finite)
+  // (a NaN bound — the closest hit so far is a rect hit at t = NaN, which rectHit does not reject: a ray
+  // in the plane of a face it runs along — makes the reference's per-axis test fail (gmin(t1, NaN) = NaN),
+  // while fmin / fmax above would drop it: decided by the exact test)
+  nan |= (t_min != t_min) | (t_max != t_max);
   const bool ok = ray_safe(r) & !nan;
   const bool yes = ok & ok_band & (U - L > band);
   const bool no = ok & ((ok_band & (L - U > band)) | (L == INFINITY) | (U == -INFINITY));
@@ -744,7 +748,7 @@ __device__ __forceinline__ void trav_redo(Trav& t, int root, double t_max, R& g,
     trav_restart_ref(t, root, t_max, true);
     return;
   }
-  if (t.best_sub == kSubMedium) {
+  if (t.best_sub == kSubMedium || t.lite) {  // (a medium's draw, or a NaN-t rect hit (trav_take): in full)
     g.rewind(walk_mark);
     trav_restart_ref(t, root, t_max, true);
     return;
@@ -813,6 +817,20 @@ __device__ __forceinline__ void trav_take(const Scene& S, Trav& t, double x, int
   } else if (x == t.closest && id != t.best_node) {  // (the same leaf twice is no tie)
     // (a tie whose records shade identically needs no redo: tie_same)
     if (!tie_same<F>(S, t, leaf, sub, plain)) t.tie = true;
+  } else if constexpr ((F & F_RECT) != 0) {
+    // A rect hit at t = NaN (a ray in the plane of a face it runs along — the Lambertian quirk's +x ray
+    // from a point exactly on a box top: rectHit rejects only t < tmin or t > tmax, Lib.hs:1014-1015).
+    // The reference keeps it as its closest hit, or replaces it, by its own tree order (every later test
+    // against a NaN bound: boxes fail, rects pass): the walk ends here (closest_up(NaN) bounds it to
+    // 2^-1074) and is redone in full in the reference's order (trav_redo).
+    // (`lite` is a redo's flag, false in a first walk: here it marks the NaN hit for trav_redo and stays
+    // set when a reference-semantics leaf later replaces the NaN and clears `tie`)
+    if (x != x) {
+      t.closest = x;
+      t.tie = true;
+      t.lite = true;
+      if constexpr (kRay32<F>) t.tmax32 = 0.0f;
+    }
   }
 }
 // A leaf: a primitive, an instance chain ending in one (its t and face only: the record is built once,
@@ -1460,7 +1478,7 @@ __device__ __forceinline__ void scatter(const Scene& S, const DMat& m, const Ray
   if (metal || (lamb && !light)) {
     const double a = g.draw(), b = g.draw();
     const double ang = 2.0 * kPi * a;
-    const double cs = cos(ang), sn = sin(ang);
+    const double cs = m_cos<R::kSL>(ang), sn = m_sin<R::kSL>(ang);
     const double z = (b * 2.0) - 1.0;                      // Metal: z = 2 zz - 1
     const double q = sqrt(metal ? 1.0 - z * z : 1.0 - b);  // Metal: r; Lambertian: z
     const double sr2 = sqrt(b);

@@ -137,6 +137,7 @@ EXPORTED = [
     "rt_debug_closest_hits", "rt_debug_math", "rt_render_work", "rt_upload_scene_ex", "rt_rebuild_bvh",
     "rt_wide_bvh", "rt_tree_stack_need", "rt_last_launch", "rt_write_pfm", "rt_debug_probe",
     "rt_prepare_scene", "rt_render_step_profile", "rt_create_multi", "rt_ctx_devices", "rt_last_frame_timing",
+    "rt_debug_exact_trace",
 ]
 
 # include/rt_wide.h: one 4-wide node (128 B)
@@ -223,6 +224,7 @@ def lib() -> C.CDLL:
             "rt_create_multi": (I, [I, P(I), P(C.c_void_p)]),
             "rt_ctx_devices": (I, [C.c_void_p, P(I), P(I), I]),
             "rt_last_frame_timing": (I, [C.c_void_p, P(rt_frame_timing)]),
+            "rt_debug_exact_trace": (I, [C.c_void_p, P(rt_camera), P(rt_render_params), P(U64), I, P(D), I, P(I)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -624,6 +626,18 @@ class Context:
         _check(lib().rt_debug_closest_hits(self._h, rays.ctypes.data_as(P(C.c_double)), rays.shape[0], tmin, tmax,
                                            seed, flags, out.ctypes.data_as(P(C.c_double))), "rt_debug_closest_hits")
         return out
+
+    def exact_trace(self, cam, params, col_gens, col: int, cap: int = 1 << 20) -> np.ndarray:
+        """rt_debug_exact_trace: tier A, column `col`'s path segments (rows of 10 doubles: row, sample, seg,
+        o, d, seed bits), as pyoracle.exact_trace records them."""
+        gi = np.ascontiguousarray(col_gens, dtype=np.uint64).reshape(-1)
+        out = np.zeros((cap, 10), dtype=np.float64)
+        n = C.c_int(0)
+        P = C.POINTER
+        _check(lib().rt_debug_exact_trace(self._h, C.byref(cam), C.byref(params), gi.ctypes.data_as(P(C.c_uint64)),
+                                          col, out.ctypes.data_as(P(C.c_double)), cap, C.byref(n)),
+               "rt_debug_exact_trace")
+        return out[: n.value].copy()
 
     def probe(self, op: str, inputs: np.ndarray, seed: int = 0, cam: Optional[rt_camera] = None) -> np.ndarray:
         """rt_debug_probe: one hot-path function per record on the device (PROBES: layouts)."""

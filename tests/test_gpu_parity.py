@@ -110,8 +110,10 @@ def test_tier_a_rng_consuming_features(gpu_ctx, name, camname, w, h, spp):
     against the oracle on every feature that consumes draws: medium draws interleaved with the walk
     (Lib.hs:1053-1080), the motion-blur time draw (Lib.hs:1253-1267, 1106-1108), Isotropic's rejection
     draws (Lib.hs:861-865), Perlin and image textures.
-    1. RT_FLAG_SHARED_LIBM (both sides evaluate sin/cos/log/atan/asin in include/rt_libm.h): bytes, linear
-       averages and end-of-stream generators bit-identical on every scene.
+    1. RT_FLAG_SHARED_LIBM (both sides evaluate sin/cos/log/atan/asin in include/rt_libm.h): bytes and
+       end-of-stream generators identical on every scene, linear averages within the tolerance (the device
+       accumulates the path's throughput forwards, the oracle in the reference's continuation order:
+       rounding only).
     2. Each side's own libm (OCML on the device, glibc in the oracle): the north-star tolerance and equal
        end generators, except where a column's serial stream meets a libm ulp that later flips a branch
        (next_week_final: thousands of fog bounces per column). There the columns that consumed the same
@@ -125,11 +127,10 @@ def test_tier_a_rng_consuming_features(gpu_ctx, name, camname, w, h, spp):
     p = rtamd.make_params(w, h, spp, 50, rtamd.RT_RNG_EXACT, flags=rtamd.RT_FLAG_SHARED_LIBM)
     rgb_g, lin_g, gens_g = gpu_ctx.render(cam, p, gens, linear=True, want_gens=True)
     rgb_o, lin_o, gens_o, _ = pyoracle.render(sc, cam, p, col_gens=gens)
-    print(f"{name} tier A, shared libm: bytes equal {float((rgb_g == rgb_o).mean()):.6f}, linear bit-identical "
-          f"{float(((lin_g == lin_o) | (np.isnan(lin_g) & np.isnan(lin_o))).mean()):.6f}, end generators equal "
-          f"{float((gens_g == gens_o).all(axis=1).mean()):.6f}")
-    assert np.array_equal(gens_g, gens_o) and np.array_equal(rgb_g, rgb_o)
-    assert np.array_equal(lin_g, lin_o, equal_nan=True)
+    ok, eq, dmax = parity(lin_g, lin_o, rgb_g, rgb_o)
+    print(f"{name} tier A, shared libm: bytes equal {eq:.6f}, channels within 1e-3 {ok:.6f}, max |d| {dmax:.3g}, "
+          f"end generators equal {float((gens_g == gens_o).all(axis=1).mean()):.6f}")
+    assert np.array_equal(gens_g, gens_o) and np.array_equal(rgb_g, rgb_o) and ok == 1.0
     p = rtamd.make_params(w, h, spp, 50, rtamd.RT_RNG_EXACT)
     rgb_g, lin_g, gens_g = gpu_ctx.render(cam, p, gens, linear=True, want_gens=True)
     rgb_o, lin_o, gens_o, _ = pyoracle.render(sc, cam, p, col_gens=gens)
@@ -443,3 +444,47 @@ def test_run_render_zip_truncation(gpu_ctx):
     assert all(np.array_equal(a, b[:41]) for a, b in zip(short, full))
     assert all(np.array_equal(a, b) for a, b in zip(rtamd.runRender(env, gens, ctx=gpu_ctx), full))
     assert all(r.shape == (0, 3) for r in rtamd.runRender(env, [], ctx=gpu_ctx))
+
+
+@pytest.mark.parametrize("parts", [("fog2", "boxes", "light"), ("boxes", "light", "fog1")])
+def test_grazing_rays_closest_hits(gpu_ctx, parts):
+    """Rays lying in the face planes of the box field (the Lambertian quirk's +x light direction from a
+    box top, nwf_parts.grazing_rays) over a world walked in the reference's order (media): exact ties
+    between neighbouring faces, rect hits at t = NaN (rectHit does not reject a NaN t, Lib.hs:1014-1015)
+    and boxes whose per-axis test fails on a NaN slab quotient (Lib.hs:798-814). The recursive walk
+    must give the oracle's closest hits with the joint slab filter as with the reference's test: the
+    joint filter's fast path drops a NaN bound (fmin / fmax), so a NaN closest hit sends it to the exact
+    test. Medium hits: t within 8 ulps (OCML vs glibc log)."""
+    from nwf_parts import grazing_rays, scene
+    sc, _ = scene(list(parts))
+    gpu_ctx.upload(sc)
+    rays = grazing_rays(sc, 1 << 15, np.random.default_rng(3))
+    ref = pyoracle.closest_hits(sc, rays, 1e-4, np.inf, seed=3)
+    mats = sc.materials["type"]
+    assert np.isnan(ref[:, 1]).sum() > 100  # (NaN-t hits occur)
+    for flags in (0, rtamd.RT_FLAG_REFERENCE_CULL):
+        got = gpu_ctx.closest_hits(rays, 1e-4, np.inf, seed=3, flags=flags)
+        same = np.all((got == ref) | (np.isnan(got) & np.isnan(ref)), axis=1)
+        med = (ref[:, 0] == 1) & (got[:, 11] == ref[:, 11]) & (mats[ref[:, 11].astype(int)] == 4)
+        close = med & (np.abs(got[:, 1] - ref[:, 1]) <= 8 * np.spacing(np.abs(ref[:, 1])))
+        print(f"{'+'.join(parts)} flags {flags}: {int((~same).sum())} rays differ, all medium t within 8 ulps: "
+              f"{bool(np.all(same | close))}")
+        assert np.all(same | close), f"{int((~(same | close)).sum())} rays differ"
+
+
+def test_exact_trace_matches_oracle(gpu_ctx):
+    """rt_debug_exact_trace against oracle_exact_trace: every path segment of a next_week_final column in
+    tier A with RT_FLAG_SHARED_LIBM — scattered ray and generator state after each segment — bit for bit
+    (the tool that localised the two round-5 tier-A divergences to one segment each)."""
+    earth = np.load(_earth_path())["rgb"]
+    sc, g1 = _scene("next_week_final", earth=earth)
+    cam = rtamd.camera("next_week", 48, 48)
+    gens = rtamd.column_gens(g1, 48)
+    gpu_ctx.upload(sc)
+    p = rtamd.make_params(48, 48, 4, 50, rtamd.RT_RNG_EXACT, flags=rtamd.RT_FLAG_SHARED_LIBM)
+    for col in (0, 17, 30):
+        a = gpu_ctx.exact_trace(cam, p, gens, col)
+        b = pyoracle.exact_trace(sc, cam, p, gens, col)
+        assert len(a) == len(b) > 48 * 4
+        assert np.array_equal(a, b, equal_nan=True), f"column {col}: first difference at record " \
+            f"{int(np.argmax(~np.all((a == b) | (np.isnan(a) & np.isnan(b)), axis=1)))}"
