@@ -251,7 +251,13 @@ def spawn_ranks(cmd, envs, poll_s=0.5):
     import threading
     # rank 0's stdout is filtered: its JSON line goes to stdout, anything else the runtime prints there
     # (gloo's connection notices) to stderr, so that stdout carries exactly one line; other ranks -> stderr
-    procs = [subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE if r == 0 else sys.stderr, text=True)
+    # (ranks above 0 write to the parent's stderr descriptor; None (inherit) when sys.stderr has no
+    # descriptor, e.g. under a capture wrapper)
+    try:
+        err_fd = sys.stderr.fileno()
+    except (AttributeError, OSError, ValueError):
+        err_fd = None
+    procs = [subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE if r == 0 else err_fd, text=True)
              for r, e in enumerate(envs)]
 
     def forward(f):
@@ -469,7 +475,8 @@ def main():
             out["roofline"] = {
                 "bound": "fp64-valu", "achieved": round(eq, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(eq / FP64_PEAK_TFLOPS, 5),
-                "traffic": traffic, "traffic_unit": "GB/s", "traffic_bytes_per_launch": tbytes,
+                "traffic": traffic, "traffic_unit": "GB/s", "traffic_bytes_per_step": tbytes,
+                "traffic_bytes_per_dispatch": round(tbytes / dispatches) if tbytes else None,
                 "kernel_dispatches_per_step": dispatches,
                 "algorithmic_offchip_bytes": off,
                 "traffic_over_algorithmic": round(tbytes / off["total"], 3) if tbytes else None,

@@ -369,9 +369,10 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
   // (the ints only acquisition and shading touch — pixel, row, the chunk's end sample, the path depth —
   // live in LDS after the stacks and Side slots, out of the walk loop's VGPRs; RT_LANE_LDS: 1 the
   // reference-order kernels, 2 every replacement-loop kernel)
-  constexpr bool kLaneLds = RT_LANE_LDS >= 2 || (RT_LANE_LDS == 1 && kRefMixed<F>);
+  constexpr int kLoop = (F & F_WIDE) ? 2 : 1;
+  constexpr bool kLaneLds = lane_lds_of(F, kLoop);
   int l_px = 0, l_row = 0, l_s_end = 0, l_depth = 0;
-  int* ex = side_p + ((F & F_FRAMES) ? side_ints_for(S.frames) : 0) * stride;
+  int* ex = side_p + side_ints_of(F, S.frames, kLoop) * stride;  // (the host sizes the LDS with the same helpers)
   int& px = kLaneLds ? ex[0] : l_px;
   int& row = kLaneLds ? ex[stride] : l_row;
   int& s_end = kLaneLds ? ex[2 * stride] : l_s_end;
@@ -614,8 +615,8 @@ __global__ void __launch_bounds__(WAVES * 256, WAVES)
   if constexpr (LEAF_LDS) S.leaves = reinterpret_cast<const rt_node*>(lds + (size_t)n_nodes * rec);
   else n_leaves = 0;
   int* stk = reinterpret_cast<int*>(lds + (size_t)n_nodes * rec + (size_t)n_leaves * sizeof(rt_node)) + threadIdx.x;
-  // (the host sizes the dynamic LDS for stack_entries stack ints + kSideInts Side ints per lane
-  // when F has F_FRAMES)
+  // (per lane: stack_entries stack ints, then side_ints_of Side slots, then lane_lds_of's 4 lane ints;
+  // launch_philox sizes the dynamic LDS with the same two helpers)
   philox_loop2<F>(A, S, stk, WAVES * 256, stk + stack_entries * WAVES * 256,
                   wave_q[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)]);
 }

@@ -395,8 +395,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   // per-sample loop 2 despite 784 B/lane of scratch (C4 35.2 vs 23.4 at 1 wave, 9.1 at 3)
   int waves = (var == kVarSpheres || loop) ? waves_target(3) : waves_target(is_full(var) ? 2 : 1);
   // Side slots after the stacks, then the 4 lane ints philox_loop2 keeps in LDS (RT_LANE_LDS)
-  const bool lane_lds = loop >= 1 && (RT_LANE_LDS >= 2 || (RT_LANE_LDS == 1 && is_full(var)));
-  const int side_ints = ((var & F_FRAMES) && loop == 1 ? side_ints_for(c->scene.frames) : 0) + (lane_lds ? 4 : 0);
+  const int side_ints = side_ints_of(var, c->scene.frames, loop) + (lane_lds_of(var, loop) ? 4 : 0);
   // LDS-staged kernel when the traversal's node array plus the stacks fit one CU's 160 KiB
   // (RTAMD_LDS=0 disables it for A/B runs).
   if (!count && !env_off("RTAMD_LDS") && (!is_full(var) || loop)) {

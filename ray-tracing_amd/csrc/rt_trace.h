@@ -561,6 +561,19 @@ __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr
 // -> 250.1 ms at 100 spp.)
 __host__ __device__ constexpr int side_ints_for(int frames) { return 14 + 2 * frames; }
 constexpr int kSideInts = side_ints_for(RT_MAX_FRAMES);
+// The replacement loop's per-lane LDS ints after the walk stack (philox_loop2's layout, launch_philox's
+// sizing — one definition for both): Side slots for the frame kernels on the binary / mixed walk (loop
+// 1), then, with RT_LANE_LDS (rt_kernels.h), the 4 lane ints (pixel, row, chunk end, depth) of the
+// reference-order kernels (RT_LANE_LDS 1) or of every replacement-loop kernel (2).
+#ifndef RT_LANE_LDS
+#define RT_LANE_LDS 1
+#endif
+__host__ __device__ constexpr int side_ints_of(unsigned var, int frames, int loop) {
+  return ((var & F_FRAMES) && loop == 1) ? side_ints_for(frames) : 0;
+}
+__host__ __device__ constexpr bool lane_lds_of(unsigned var, int loop) {
+  return loop >= 1 && (RT_LANE_LDS >= 2 || (RT_LANE_LDS == 1 && (var & (F_MEDIA | F_FRAMES)) != 0));
+}
 struct Side {
   int* p;
   int stride;
