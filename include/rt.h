@@ -68,7 +68,9 @@ enum rt_node_type {
  *   CUBOID         f = min xyz, max xyz; a = material (the six rects are implied, Lib.hs:599-604)
  *   TRANSLATE      f[0..2] = offset; a = child
  *   ROTATE         f[0] = sin theta, f[1] = cos theta; a = child; b = axis (0 X, 1 Y, 2 Z)
- *   CONSTANT_MEDIUM f[0] = negative inverse density; a = boundary; b = phase material
+ *   CONSTANT_MEDIUM f[0] = negative inverse density; a = boundary; b = phase material; f[1] = 0, or the
+ *                  occurrence key + 1 of an unfolded medium record (rt_rebuild_bvh output; see
+ *                  RT_RNG_PHILOX: the upload keys every medium occurrence of the caller's tree)
  * For every type c = htblSize of the node (Lib.hs:662-671): BVH its size, Translate/Rotate
  * the size of the child, Unhittable 0, everything else 1. (World-only BVH nodes appended by the
  * device-side rebuild carry 0x40000000 | split axis instead; they never occur in a lights tree.)
@@ -178,6 +180,15 @@ typedef struct rt_camera {
  *                from 0. (The chunks are the device's work-items; a definition fixed by
  *                (width, height, spp) keeps the image independent of scheduling and shard
  *                count.) Embarrassingly parallel.
+ *                ConstantMedium (src/Lib.hs:1053-1080) in tier B: its draw is not the stream's next
+ *                but the first word of the block at counter {stream words consumed so far, sample,
+ *                pixel_id, 2^31 | key}, key = the occurrence's preorder rank among the medium
+ *                occurrences of the caller's world tree (BVH left child first, into Translate/Rotate;
+ *                one occurrence per path) or f[1] - 1 when set; and its candidate hit is computed over
+ *                the boundary's whole inside, then accepted like a leaf's at t <= the bound. The
+ *                closest hit is then the least t over every leaf in any walk order (exact ties are
+ *                resolved in the reference's order), so media worlds walk re-bounded trees too.
+ *                Tier A keeps the reference's own medium: the stream's next draw, under the walk's bound.
  */
 #define RT_RNG_EXACT 0
 #define RT_RNG_PHILOX 1
@@ -361,9 +372,11 @@ typedef struct rt_frame_timing {
 int rt_last_frame_timing(rt_ctx* ctx, rt_frame_timing* out);
 void rt_destroy(rt_ctx* ctx);
 /* Copy a scene to device memory (caller-owned desc; arrays are copied). Validates it.
- * By default a world tree without ConstantMedium is re-bounded by a binned-SAH BVH over the same
- * leaves for traversal (closest hits are tree-independent except for exact ties);
- * the lights tree is always the caller's. */
+ * Every medium occurrence of the world tree becomes its own keyed record (RT_RNG_PHILOX above), and by
+ * default the world tree is re-bounded by a binned-SAH BVH over the same leaves, media and instance
+ * frames included (the trees inside frames re-bounded in their own coordinates), for traversal (closest
+ * hits are tree-independent except for exact ties, which are redone on the caller's tree; DESIGN.md
+ * §3); the lights tree is always the caller's. */
 int rt_upload_scene(rt_ctx* ctx, const rt_scene_desc* desc);
 #define RT_UPLOAD_REFERENCE_BVH 1u /* traverse the caller's (makeBVH's) world tree as is */
 int rt_upload_scene_ex(rt_ctx* ctx, const rt_scene_desc* desc, uint32_t flags);

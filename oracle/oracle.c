@@ -137,6 +137,13 @@ static inline uint64_t rng_word(Rng* g) {
 }
 /* randomDoubleM (src/Lib.hs:1119-1125) */
 static inline double D(Rng* g) { return word_to_draw(rng_word(g)); }
+/* Tier B, a medium occurrence's draw: the first word of the Philox block at counter {words of the sample's
+   stream consumed so far (the walk consumes none, so this names the walk), sample, pixel, 2^31 | key}. */
+static inline double keyed_draw(const Rng* g, uint32_t key) {
+    uint32_t ctr[4] = {2u * g->pair - (uint32_t)g->have_spare, g->sample, g->pid, 0x80000000u | key}, o[4];
+    philox4x32_10(ctr, g->key, o);
+    return word_to_draw((uint64_t)o[0] | ((uint64_t)o[1] << 32));
+}
 /* randomDoubleRM (src/Lib.hs:1127-1130) */
 static inline double DR(Rng* g, double mn, double mx) { double rd = D(g); return mn + (mx - mn) * rd; }
 
@@ -217,7 +224,23 @@ typedef struct {
     const rt_camera* cam;
     int width, height, spp, max_depth;
     int64_t* counters; /* per-thread, optional */
+    const uint32_t* medcount; /* medium occurrences under each node (tier-B medium keys), or NULL */
 } Ctx;
+
+/* Medium occurrences under each node of the world DAG (children precede parents): a BVH node's are its
+   children's, a Translate/Rotate's its child's, a ConstantMedium is one. The walk keys a medium occurrence
+   by its preorder rank (hit's `mb`: the occurrences left of it), unless the record carries its key + 1 in
+   f[1] (an unfolded array, rt_rebuild_bvh). Caller frees. */
+static uint32_t* medium_counts(const rt_scene_desc* d) {
+    uint32_t* m = (uint32_t*)calloc((size_t)d->n_nodes, sizeof(uint32_t));
+    for (int i = 0; i < d->n_nodes; ++i) {
+        const rt_node* n = &d->nodes[i];
+        if (n->type == RT_NODE_CONSTANT_MEDIUM) m[i] = 1;
+        else if (n->type == RT_NODE_BVH && n->a >= 0 && n->a < i && n->b >= 0 && n->b < i) m[i] = m[n->a] + m[n->b];
+        else if ((n->type == RT_NODE_TRANSLATE || n->type == RT_NODE_ROTATE) && n->a >= 0 && n->a < i) m[i] = m[n->a];
+    }
+    return m;
+}
 
 enum { C_WORLD_QUERIES, C_BOX_TESTS, C_SPHERE_TESTS, C_RECT_TESTS, C_OTHER_PRIMS, C_SCATTERS,
        C_DRAWS, C_SAMPLES, C_LIGHT_QUERIES, C_NCOUNTERS };
@@ -373,7 +396,7 @@ static V3 unrotate_point(int axis, double s, double c, V3 p) {
     return v3(c * p.x + s * p.y, -s * p.x + c * p.y, p.z);
 }
 
-static int hit(const Ctx* c, int id, Ray r, double t_min, double t_max, Rng* g, Hit* h) {
+static int hit(const Ctx* c, int id, Ray r, double t_min, double t_max, Rng* g, Hit* h, uint32_t mb) {
     if (id < 0) return 0; /* Unhittable */
     const rt_node* n = &c->s->nodes[id];
     switch (n->type) {
@@ -381,9 +404,10 @@ static int hit(const Ctx* c, int id, Ray r, double t_min, double t_max, Rng* g, 
         CNT(c, C_BOX_TESTS);
         if (!box_ray_intersect(n->f, r, t_min, t_max)) return 0;
         Hit hl;
-        if (!hit(c, n->a, r, t_min, t_max, g, &hl)) return hit(c, n->b, r, t_min, t_max, g, h);
+        const uint32_t mb_right = mb + (c->medcount ? c->medcount[n->a] : 0);
+        if (!hit(c, n->a, r, t_min, t_max, g, &hl, mb)) return hit(c, n->b, r, t_min, t_max, g, h, mb_right);
         Hit hr;
-        if (hit(c, n->b, r, t_min, hl.t, g, &hr)) *h = hr; else *h = hl;
+        if (hit(c, n->b, r, t_min, hl.t, g, &hr, mb_right)) *h = hr; else *h = hl;
         return 1;
     }
     case RT_NODE_CUBOID: { /* Lib.hs:989-1004: foldr closerHit, full range for every face */
@@ -415,7 +439,7 @@ static int hit(const Ctx* c, int id, Ray r, double t_min, double t_max, Rng* g, 
         V3 off = vload(n->f);
         Ray mr = {vsub(r.o, off), r.d, r.tm};
         Hit ch;
-        if (!hit(c, n->a, mr, t_min, t_max, g, &ch)) return 0;
+        if (!hit(c, n->a, mr, t_min, t_max, g, &ch, mb)) return 0;
         *h = ch;
         face_normal(mr, ch.n, &h->ff, &h->n);
         h->p = vadd(ch.p, off);
@@ -427,7 +451,7 @@ static int hit(const Ctx* c, int id, Ray r, double t_min, double t_max, Rng* g, 
         double s = n->f[0], co = n->f[1];
         Ray rr = {unrotate_point(ax, s, co, r.o), unrotate_point(ax, s, co, r.d), r.tm};
         Hit ch;
-        if (!hit(c, n->a, rr, t_min, t_max, g, &ch)) return 0;
+        if (!hit(c, n->a, rr, t_min, t_max, g, &ch, mb)) return 0;
         *h = ch;
         h->p = rotate_point(ax, s, co, ch.p);
         face_normal(rr, rotate_point(ax, s, co, ch.n), &h->ff, &h->n);
@@ -436,18 +460,24 @@ static int hit(const Ctx* c, int id, Ray r, double t_min, double t_max, Rng* g, 
     case RT_NODE_CONSTANT_MEDIUM: { /* Lib.hs:1053-1080 */
         CNT(c, C_OTHER_PRIMS);
         Hit h1, h2;
-        if (!hit(c, n->a, r, -INFINITY, INFINITY, g, &h1)) return 0;
-        if (!hit(c, n->a, r, h1.t + EPSILON, INFINITY, g, &h2)) return 0;
+        if (!hit(c, n->a, r, -INFINITY, INFINITY, g, &h1, 0)) return 0;
+        if (!hit(c, n->a, r, h1.t + EPSILON, INFINITY, g, &h2, 0)) return 0;
+        /* Tier B (Philox streams): the draw is keyed by (walk, occurrence) and the candidate computed over
+           the boundary's whole inside, then bounded like any leaf (newt <= t_max): the closest hit no longer
+           depends on the order media are visited in. Tier A: the reference's own, the
+           stream's next draw, made only when the inside meets [t_min, t_max]. */
+        const int keyed = g->mode == RT_RNG_PHILOX;
         double rec1tp = gmax(t_min, h1.t);
-        double rec2t = gmin(t_max, h2.t);
+        double rec2t = keyed ? h2.t : gmin(t_max, h2.t);
         if (rec1tp >= rec2t) return 0;
         double rec1t = rec1tp < 0 ? 0 : rec1tp;
         double ray_length = vlength(r.d);
         double dist_inside = (rec2t - rec1t) * ray_length;
-        double rnd = D(g);
+        double rnd = keyed ? keyed_draw(g, n->f[1] >= 1.0 ? (uint32_t)(n->f[1] - 1.0) : mb) : D(g);
         double hit_dist = n->f[0] * o_log(rnd);
         if (hit_dist > dist_inside) return 0;
         double newt = rec1t + (hit_dist / ray_length);
+        if (keyed && !(newt <= t_max)) return 0;
         h->t = newt;
         h->p = at(r, newt);
         h->n = v3(1, 0, 0);
@@ -480,7 +510,7 @@ static double htbl_pdf_value(const Ctx* c, int id, V3 origin, V3 v, Rng* g) {
     CNT(c, C_LIGHT_QUERIES);
     Ray r = {origin, v, 0.0};
     Hit hh;
-    if (!hit(c, id, r, EPSILON, INFINITY, g, &hh)) return 0.0;
+    if (!hit(c, id, r, EPSILON, INFINITY, g, &hh, 0)) return 0.0;
     const rt_node* n = &c->s->nodes[id];
     if (n->type == RT_NODE_RECT_XZ) {
         double x0 = n->f[0], x1 = n->f[1], z0 = n->f[2], z1 = n->f[3];
@@ -638,7 +668,7 @@ static V3 ray_color(const Ctx* c, Ray r, int d, Rng* g) {
     if (d <= 0) { trace_seg(c->max_depth - d, 1, r, g); return v3(0, 0, 0); }
     CNT(c, C_WORLD_QUERIES);
     Hit h;
-    if (!hit(c, c->s->world_root, r, EPSILON, INFINITY, g, &h)) {
+    if (!hit(c, c->s->world_root, r, EPSILON, INFINITY, g, &h, 0)) {
         trace_seg(c->max_depth - d, 1, r, g);
         return vload(c->s->background);
     }
@@ -755,6 +785,7 @@ int oracle_render_rows(const rt_scene_desc* scene, const rt_camera* cam, const r
     if ((p->flags & RT_FLAG_SHARED_LIBM) && p->rng_mode != RT_RNG_EXACT) return -1; /* (as rt_render) */
     const int W = p->width, H = p->height;
     g_shared_libm = (p->flags & RT_FLAG_SHARED_LIBM) != 0;
+    uint32_t* mc = medium_counts(scene);
     if (counters) memset(counters, 0, sizeof(int64_t) * C_NCOUNTERS);
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
@@ -767,7 +798,7 @@ int oracle_render_rows(const rt_scene_desc* scene, const rt_camera* cam, const r
         {
             int64_t cnt[C_NCOUNTERS] = {0};
             double* uvbuf = (double*)malloc(sizeof(double) * 2 * (size_t)p->spp);
-            Ctx c = {scene, cam, W, H, p->spp, p->max_depth, counters ? cnt : NULL};
+            Ctx c = {scene, cam, W, H, p->spp, p->max_depth, counters ? cnt : NULL, mc};
 #pragma omp for schedule(dynamic, 1)
             for (int x = 0; x < W; ++x) {
                 Rng g;
@@ -794,7 +825,7 @@ int oracle_render_rows(const rt_scene_desc* scene, const rt_camera* cam, const r
 #pragma omp parallel
         {
             int64_t cnt[C_NCOUNTERS] = {0};
-            Ctx c = {scene, cam, W, H, p->spp, p->max_depth, counters ? cnt : NULL};
+            Ctx c = {scene, cam, W, H, p->spp, p->max_depth, counters ? cnt : NULL, mc};
 #pragma omp for schedule(dynamic, 16)
             for (int64_t i = 0; i < npx; ++i) {
                 int row = row0 + (int)(i / W), x = (int)(i % W);
@@ -810,6 +841,7 @@ int oracle_render_rows(const rt_scene_desc* scene, const rt_camera* cam, const r
         }
     }
     g_shared_libm = 0;
+    free(mc);
     return 0;
 }
 
@@ -821,7 +853,7 @@ int oracle_exact_trace(const rt_scene_desc* scene, const rt_camera* cam, const r
                        const uint64_t* col_gens, int col, double* out, int cap, int* out_n) {
     if (!scene || !cam || !p || !col_gens || col < 0 || col >= p->width || !out || cap < 0) return -1;
     g_shared_libm = (p->flags & RT_FLAG_SHARED_LIBM) != 0;
-    Ctx c = {scene, cam, p->width, p->height, p->spp, p->max_depth, NULL};
+    Ctx c = {scene, cam, p->width, p->height, p->spp, p->max_depth, NULL, NULL};
     double* uvbuf = (double*)malloc(sizeof(double) * 2 * (size_t)p->spp);
     Rng g;
     memset(&g, 0, sizeof g);
@@ -867,7 +899,8 @@ int oracle_num_counters(void) { return C_NCOUNTERS; }
 /* Closest hit of n world rays (7 doubles each) — same layout as rt_debug_closest_hits. */
 int oracle_closest_hits(const rt_scene_desc* scene, const double* rays, int n, double tmin, double tmax,
                         uint64_t seed, double* out) {
-    Ctx c = {scene, NULL, 0, 0, 0, 0, NULL};
+    uint32_t* mc = medium_counts(scene);
+    Ctx c = {scene, NULL, 0, 0, 0, 0, NULL, mc};
     for (int i = 0; i < n; ++i) {
         const double* q = rays + 7 * i;
         Ray r = {v3(q[0], q[1], q[2]), v3(q[3], q[4], q[5]), q[6]};
@@ -880,13 +913,14 @@ int oracle_closest_hits(const rt_scene_desc* scene, const double* rays, int n, d
         Hit h;
         double* o = out + 12 * i;
         memset(o, 0, sizeof(double) * 12);
-        if (hit(&c, scene->world_root, r, tmin, tmax, &g, &h)) {
+        if (hit(&c, scene->world_root, r, tmin, tmax, &g, &h, 0)) {
             o[0] = 1; o[1] = h.t;
             o[2] = h.p.x; o[3] = h.p.y; o[4] = h.p.z;
             o[5] = h.n.x; o[6] = h.n.y; o[7] = h.n.z;
             o[8] = h.u; o[9] = h.v; o[10] = h.ff; o[11] = h.mat;
         }
     }
+    free(mc);
     return 0;
 }
 
@@ -914,7 +948,7 @@ int oracle_probe(const rt_scene_desc* scene, const rt_camera* cam, int op, const
                  double* out) {
     static const int IN[5] = {18, 3, 6, 6, 2}, OUT[5] = {14, 4, 2, 3, 8};
     if (!scene || op < 0 || op > 4 || n < 0 || (op == 4 && !cam)) return -1;
-    Ctx c = {scene, cam, 0, 0, 0, 0, NULL};
+    Ctx c = {scene, cam, 0, 0, 0, 0, NULL, NULL};
     for (int i = 0; i < n; ++i) {
         const double* q = in + (size_t)IN[op] * i;
         double* o = out + (size_t)OUT[op] * i;

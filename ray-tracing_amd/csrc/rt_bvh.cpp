@@ -7,9 +7,10 @@
 // depend on the tree's shape except for exact ties (two primitives at bit-identical t): every
 // leaf's own hit test is unchanged, and boxes only cull. So the device may traverse a better
 // tree over the SAME leaves (spheres, rects, cuboids, instance sub-DAGs, moving spheres, each
-// bounded exactly as boundingBox bounds it). Media keep the reference tree: the order in which
-// media are visited fixes their RNG draws. The lights tree is never touched (its BVH sizes weight
-// htblPdfValue / htblRandom, src/Lib.hs:694-723).
+// bounded exactly as boundingBox bounds it). Media are leaves too: their tier-B draws are keyed per
+// occurrence (unfold_media) and their candidate hit does not depend on the walk's bound (DESIGN.md
+// §3.2). The lights tree is never touched (its BVH sizes weight htblPdfValue / htblRandom,
+// src/Lib.hs:694-723).
 #include <algorithm>
 #include <array>
 #include <cstdlib>
@@ -371,13 +372,17 @@ int rebuild_world_bvh(std::vector<rt_node>& nodes, int root) {
 
 namespace {
 
+bool kMediaSkeleton = false;  // (RTAMD_MEDIA_SKELETON=1, read by rebuild_media_skeleton)
+
 // rebuild_media_skeleton's recursion: the id that replaces node `id` (itself when unchanged).
 int skeleton(std::vector<rt_node>& nodes, int id, int depth) {
   if (depth > 512) return id;
   const rt_node n = nodes[id];  // (a copy: `nodes` grows)
   if (n.type == RT_NODE_BVH) {
-    if (!has_media(nodes, id)) {
-      // a media-free subtree: its leaves, instance frames first rebuilt inside, re-bounded by SAH
+    // (round 5: media are leaves too, keyed per occurrence by unfold_media: no skeleton is kept above
+    // them; RTAMD_MEDIA_SKELETON=1 keeps it, for A/B runs — same images, since the draws are keyed)
+    if (!kMediaSkeleton || !has_media(nodes, id)) {
+      // a subtree: its leaves, instance frames first rebuilt inside, re-bounded by SAH
       std::vector<int> leaves;
       std::vector<char> seen(nodes.size(), 0);
       collect_leaves(nodes, id, leaves, seen);
@@ -420,6 +425,8 @@ int skeleton(std::vector<rt_node>& nodes, int id, int depth) {
 // does not depend on its shape except for exact ties, which the walk detects (rt_trace.h). Returns
 // the new root (== root when nothing changed).
 int rebuild_media_skeleton(std::vector<rt_node>& nodes, int root) {
+  const char* ms = std::getenv("RTAMD_MEDIA_SKELETON");
+  kMediaSkeleton = ms && ms[0] == '1';
   const size_t n0 = nodes.size();
   const int r = skeleton(nodes, root, 0);
   std::vector<int> need;
@@ -599,9 +606,71 @@ bool build_wide_bvh(const std::vector<rt_node>& nodes, int root, std::vector<rt_
   return true;
 }
 
-// The world tree the device walks, as rt_upload_scene builds it: worlds with ConstantMedium or
-// instance frames (Translate/Rotate over a BVH) keep their skeleton (rebuild_media_skeleton;
-// RTAMD_SKELETON=0: the caller's tree as is), the others are rebuilt whole (rebuild_world_bvh).
+// Tier-B medium draws are keyed by the medium's occurrence (include/rt.h): the preorder
+// rank of the occurrence among the medium occurrences of the caller's tree walked from the world root
+// (BVH left child before right, into Translate/Rotate children; a medium's boundary holds none). A DAG
+// can reach one ConstantMedium record along several paths (BVHNode h h, src/Lib.hs:948; shared
+// sub-trees), and each occurrence draws with its own key. So every record on a path to a medium is
+// copied once per path (appended, children before parents) and each medium copy carries key + 1 in
+// f[1]; media-free sub-trees stay shared. A medium already keyed (f[1] >= 1: an unfolded array uploaded
+// again) keeps its key. Returns the unfolded root (`root` itself when no medium lies below it); -1 when
+// the unfolded tree would be too large (more than 2^22 records) or is not a DAG with children first.
+int unfold_media(std::vector<rt_node>& nodes, int root) {
+  const int n0 = (int)nodes.size();
+  if (root < 0 || root >= n0) return -1;
+  std::vector<signed char> memo(n0, -1);
+  bool ok = true;
+  std::function<bool(int, int)> has = [&](int id, int depth) -> bool {
+    if (id < 0 || id >= n0 || depth > 4096) {
+      ok = false;
+      return false;
+    }
+    if (memo[id] >= 0) return memo[id] != 0;
+    const rt_node& x = nodes[id];
+    bool m = false;
+    if (x.type == RT_NODE_CONSTANT_MEDIUM) m = true;
+    else if (x.type == RT_NODE_BVH) m = (x.a < id && x.b < id) ? (has(x.a, depth + 1) | has(x.b, depth + 1)) : (ok = false);
+    else if (x.type == RT_NODE_TRANSLATE || x.type == RT_NODE_ROTATE) m = x.a < id ? has(x.a, depth + 1) : (ok = false);
+    memo[id] = m ? 1 : 0;
+    return m;
+  };
+  if (!has(root, 0)) return ok ? root : -1;
+  uint32_t rank = 0;
+  std::function<int(int)> copy = [&](int id) -> int {
+    if (!ok || !has(id, 0)) return id;
+    if ((int)nodes.size() >= (1 << 22)) {
+      ok = false;
+      return id;
+    }
+    rt_node x = nodes[id];  // (a copy: `nodes` grows)
+    if (x.type == RT_NODE_CONSTANT_MEDIUM) {
+      if (!(x.f[1] >= 1.0)) x.f[1] = (double)rank + 1.0;
+      ++rank;
+    } else if (x.type == RT_NODE_BVH) {
+      const int a = copy(x.a);
+      const int b = copy(x.b);
+      x.a = a;
+      x.b = b;
+    } else {  // Translate / Rotate
+      x.a = copy(x.a);
+    }
+    nodes.push_back(x);
+    return (int)nodes.size() - 1;
+  };
+  const int r = copy(root);
+  if (!ok) {
+    nodes.resize(n0);
+    return -1;
+  }
+  return r;
+}
+
+// The world tree the device walks, as rt_upload_scene builds it (after unfold_media): worlds with
+// instance frames (Translate/Rotate over a BVH) or media are re-bounded by SAH over their leaves —
+// media are leaves like any other, their tier-B draws being keyed by occurrence and their candidate hit
+// computed without the walk's bound (order-independent) — with every tree inside a frame
+// re-bounded in the frame's coordinates (rebuild_media_skeleton; RTAMD_SKELETON=0: the caller's tree
+// as is); the others are rebuilt whole (rebuild_world_bvh).
 int rebuild_for_device(std::vector<rt_node>& nodes, int root) {
   bool media = false, frames = false;
   std::vector<char> seen(nodes.size(), 0);
@@ -636,7 +705,12 @@ extern "C" int rt_rebuild_bvh(const rt_scene_desc* in, rt_node* out_nodes, int c
     return RT_E_INVALID;
   }
   std::vector<rt_node> nodes(in->nodes, in->nodes + in->n_nodes);
-  const int root = rt::rebuild_for_device(nodes, in->world_root);
+  const int unfolded = rt::unfold_media(nodes, in->world_root);
+  if (unfolded < 0) {
+    rt::set_error("rt_rebuild_bvh: the world tree is not a DAG with children first, or unfolds too large");
+    return RT_E_INVALID;
+  }
+  const int root = rt::rebuild_for_device(nodes, unfolded);
   *out_n = (int)nodes.size();
   *out_root = root;
   if (out_nodes) {

@@ -188,6 +188,7 @@ __device__ __forceinline__ double word_to_draw(uint64_t w) {
 template <bool SL = false>
 struct RngExactT {
   static constexpr bool kSL = SL;
+  static constexpr bool kKeyed = false;  // media draw from the stream, in the walk's order (the reference's)
   uint64_t seed, gamma;
   __device__ __forceinline__ void reserve(int) {}
   __device__ __forceinline__ double draw() {
@@ -220,6 +221,8 @@ __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) 
 // Philox evaluation.) The sequence of words is the stream's, whatever the reserve points.
 struct RngPhilox {
   static constexpr bool kSL = false;
+  // media draw keyed by (walk, occurrence): keyed() below, not from the stream
+  static constexpr bool kKeyed = true;
   uint32_t k0, k1, pid, sample, pair;
   uint32_t n;  // buffered words
   uint64_t w0, w1, w2, w3;
@@ -255,17 +258,17 @@ struct RngPhilox {
       n += 2;
     }
   }
-  // Words of this stream consumed so far (word i is word i % 2 of block i / 2), and the state after
-  // exactly `c` of them: a walk that has to be redone can repeat its draws.
+  // Words of this stream consumed so far (word i is word i % 2 of block i / 2).
   __device__ __forceinline__ uint32_t consumed() const { return 2u * pair - n; }
-  __device__ __forceinline__ void rewind(uint32_t c) {
-    pair = c >> 1;
-    n = 0;
-    if (c & 1u) {
-      uint64_t x;
-      block(x, w0);
-      n = 1;
-    }
+  // A medium occurrence's draw (tier B): the first word of the Philox block at counter {words of this
+  // sample's stream consumed so far, sample, pixel, 2^31 | key}, key = the occurrence's key (rt_bvh.cpp
+  // unfold_media). A walk consumes no stream words, so the counter names the walk (the path's position in
+  // its stream) and the key the occurrence: the draw does not depend on the order media are visited in.
+  // Word 3 >= 2^31 keeps these blocks apart from the stream's (word 3 = 0).
+  __device__ __forceinline__ double keyed(uint32_t key) const {
+    uint32_t c[4] = {consumed(), sample, pid, 0x80000000u | key};
+    philox(c, k0, k1);
+    return word_to_draw((uint64_t)c[0] | ((uint64_t)c[1] << 32));
   }
   __device__ __forceinline__ double draw() {
     if (n == 0) block(w0, w1), n = 2;  // not reserved: compute here

@@ -356,9 +356,6 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
 
   long long w = -1;  // the current chunk's slot in A.partial
   bool done = false, walking = false, ready = false;
-  // (worlds walked in the reference's order) the stream position at the start of the walk: a walk
-  // redone for an exact tie repeats its media draws
-  uint32_t walk_mark = 0;
   // wq[0..1]: the wave's claimed, not yet handed out work-items [next, end), in LDS (lanes that
   // are walking skip the acquisition code, so a per-lane copy would go stale); indices are < 2^32
   // (launch_philox checks)
@@ -416,7 +413,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     if (ready && (t.tie || t.lite) && !t.redo) {
       ready = false;
       if constexpr ((F & F_COUNT) != 0) ++cnt.ties;
-      trav_redo<F>(t, S.world_ref, INFINITY, g, walk_mark);
+      trav_redo<F>(t, S.world_ref, INFINITY);
       // (the redo's binary box tests need 1/d: recomputed here, the same values, so that the 4-wide
       // walk need not carry Trav::ray.inv)
       if constexpr ((F & F_WIDE) != 0) t.ray = prep(plain(t.ray));
@@ -521,11 +518,6 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
       trav_begin<F>(t, plain(t.ray), S.world, kEps, INFINITY);
       // worlds with media or frames: the reference's order over the re-bounded skeleton
       if (S.ref_walk) trav_restart_ref(t, S.world, INFINITY);
-      if constexpr (kRefMixed<F>) walk_mark = g.consumed();
-      // (media draw inside the walk: top the FIFO up here, where the starting lanes run together,
-      // so that a medium's draw does not evaluate Philox inside a divergent walk step; the words and
-      // their order are the stream's, and consumed() is unchanged)
-      if constexpr ((F & F_MEDIA) != 0) g.reserve(2);
       walking = true;
     }
     if (!walking) break;  // this lane is finished; the rest of the wave carries on without it
@@ -737,7 +729,7 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
     bool walking = true;
     walk_until<F>(S, t, walking, tmin, stk, RT_BLOCK, joint != 0, 0, 0, cnt, g, side);
     if (t.tie || t.lite) {
-      trav_redo<F>(t, S.world_ref, tmax, g, 0u);
+      trav_redo<F>(t, S.world_ref, tmax);
       while (trav_step<F>(S, t, tmin, stk, RT_BLOCK, joint != 0, cnt, g, side)) {
       }
     }

@@ -9,6 +9,7 @@
 #endif
 
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstdlib>
 #include <functional>
@@ -21,6 +22,7 @@ using namespace rtd;
 namespace rt {
 int rebuild_world_bvh(std::vector<rt_node>& nodes, int root);
 int rebuild_for_device(std::vector<rt_node>& nodes, int root);
+int unfold_media(std::vector<rt_node>& nodes, int root);
 bool build_wide_bvh(const std::vector<rt_node>& nodes, int root, std::vector<rt_wnode>& out, int* stack_need);
 }  // namespace rt
 
@@ -89,6 +91,9 @@ struct Validator {
           if (!chain_prim[x.a])
             return unsup("ConstantMedium boundary must be a primitive or a Translate/Rotate chain of one");
           if (x.b < 0 || x.b >= d->n_materials) return fail("medium material out of range");
+          // f[1]: 0, or the occurrence key + 1 of a medium already unfolded (rt_rebuild_bvh output)
+          if (!(x.f[1] == 0.0 || (x.f[1] >= 1.0 && x.f[1] <= 2147483648.0 && x.f[1] == std::floor(x.f[1]))))
+            return fail("ConstantMedium f[1] must be 0 or an occurrence key + 1 in [1, 2^31]");
           break;
         case RT_NODE_UNHITTABLE:
         case RT_NODE_EXT:
@@ -304,15 +309,21 @@ int prepare_scene(const rt_scene_desc* din, uint32_t flags, PreparedScene& P) {
   rt_scene_desc dd = *din;
   const char* env = std::getenv("RTAMD_REFERENCE_BVH");
   const bool keep = (flags & RT_UPLOAD_REFERENCE_BVH) || (env && env[0] == '1');
+  // validate the original first so that unfolding and the rebuild only ever see well-formed DAGs
+  Validator v0{din};
+  if (!v0.run()) return fail_with(v0.code, "rt_upload_scene: " + v0.err);
+  // every medium occurrence its own record, keyed (tier-B draws; rt_bvh.cpp unfold_media): the caller's
+  // tree as the walks take it in the reference's order (tier A, exact-tie redos)
+  const int unfolded = unfold_media(nodes, din->world_root);
+  if (unfolded < 0)
+    return fail_with(RT_E_UNSUPPORTED, "rt_upload_scene: the world's medium occurrences unfold to more than 2^22 records");
+  dd.world_root = unfolded;
   if (!keep) {
-    // validate the original first so the rebuild only ever sees well-formed DAGs
-    Validator v0{din};
-    if (!v0.run()) return fail_with(v0.code, "rt_upload_scene: " + v0.err);
     // Worlds without media or instance frames: a whole new tree over the same leaves (exact ties are
-    // redone on the caller's tree). Worlds walked in the reference's order (media draws, frames):
-    // the skeleton above the media stays, the media-free subtrees below it (and the trees inside
-    // frames) are re-bounded; RTAMD_SKELETON=0 keeps the caller's tree as is.
-    dd.world_root = rebuild_for_device(nodes, din->world_root);
+    // redone on the caller's tree). Worlds with media or frames: the same over leaves that include the
+    // media and the frames, with the trees inside frames re-bounded too; RTAMD_SKELETON=0 keeps the
+    // caller's tree as is.
+    dd.world_root = rebuild_for_device(nodes, unfolded);
   }
   if ((int)nodes.size() >= RT_ISMED)
     return fail_with(RT_E_INVALID, "rt_upload_scene: too many nodes (ids must stay below 2^26)");
@@ -352,7 +363,7 @@ int prepare_scene(const rt_scene_desc* din, uint32_t flags, PreparedScene& P) {
   }
   if (d->image_pool_bytes < 0 || (d->image_pool_bytes > 0 && !d->image_pool))
     return fail_with(RT_E_INVALID, "rt_upload_scene: image_pool is null but image_pool_bytes > 0");
-  P.rebuilt_bvh = dd.world_root != din->world_root;
+  P.rebuilt_bvh = dd.world_root != unfolded;
   // BVH children that are BVH nodes carry RT_ISBOX in the device copy, media RT_ISMED (every walk masks
   // them off), so that the walks' step scheduling knows a node's kind without loading it
   const std::vector<rt_node> untagged = v.nodes;  // (the mixed walk's wide trees are built from it)
@@ -373,15 +384,15 @@ int prepare_scene(const rt_scene_desc* din, uint32_t flags, PreparedScene& P) {
     }
   P.nodes = std::move(v.nodes);
   P.world = d->world_root | kind_tag(d->world_root);
-  P.world_ref = din->world_root | kind_tag(din->world_root);
+  P.world_ref = unfolded | kind_tag(unfolded);
   P.world_root = d->world_root;
   P.lights = d->lights_root;
   P.features = scene_features(d);
   // (tie redo walks the caller's tree: size the stacks for both)
-  P.stack_need = std::max(v.stack_need[d->world_root], v.stack_need[din->world_root]);
+  P.stack_need = std::max(v.stack_need[d->world_root], v.stack_need[unfolded]);
   // The replacement loop takes every world whose frames nest at most RT_MAX_FRAMES deep (its Side
   // slots); worlds with media or frames walk the caller's tree in the reference's order.
-  P.frame_depth = std::max(v.frame_depth[d->world_root], v.frame_depth[din->world_root]);
+  P.frame_depth = std::max(v.frame_depth[d->world_root], v.frame_depth[unfolded]);
   const bool frames = v.frame_depth[d->world_root] > 0;
   P.replace_ok = v.frame_depth[d->world_root] <= RT_MAX_FRAMES;
   P.ref_walk = (P.features & F_MEDIA) || frames;
@@ -409,11 +420,11 @@ int prepare_scene(const rt_scene_desc* din, uint32_t flags, PreparedScene& P) {
         }
       P.wnodes = std::move(wide);
       P.leaves = std::move(leaves);
-      P.wide_stack_need = std::max(need, v.stack_need[din->world_root]);
+      P.wide_stack_need = std::max(need, v.stack_need[unfolded]);
     }
   }
   if (P.replace_ok && P.ref_walk && !env_off("RTAMD_MIXW"))
-    mixed_wide_trees(P, nodes, untagged, d->world_root, v.stack_need[din->world_root]);
+    mixed_wide_trees(P, nodes, untagged, d->world_root, v.stack_need[unfolded]);
   return RT_OK;
 }
 

@@ -414,8 +414,15 @@ __device__ __forceinline__ bool chain_tx(const Scene& S, int id, const RayX& rx,
   return prim_t<F>(S, &S.nodes[id], rx, t_min, t_max, t, sub);
 }
 
+// A medium record's occurrence key (rt_bvh.cpp unfold_media: f[1] = key + 1 on the device copy).
+__device__ __forceinline__ uint32_t medium_key(const rt_node* n) { return (uint32_t)(n->f[1] - 1.0); }
+
 // hit ConstantMedium (Lib.hs:1053-1080). The boundary is a primitive chain (host-validated); only
-// the two boundary hits' t are used.
+// the two boundary hits' t are used. Tier A (R = RngExactT) follows the reference exactly: the draw is
+// the column stream's next, made only when the boundary's inside meets [t_min, t_max]. Tier B (RngPhilox,
+// kKeyed) redefines the draw as keyed by the walk and the occurrence, and the candidate as unbounded:
+// the closest hit is then the least t over all leaves whatever the order (exact ties aside), so media
+// worlds walk re-bounded trees like any other.
 template <unsigned F, class R>
 __device__ inline bool medium_hit(const Scene& S, const rt_node* n, const RayX& rx, double t_min, double t_max, R& g,
                                   Hit& h) {
@@ -424,15 +431,20 @@ __device__ inline bool medium_hit(const Scene& S, const rt_node* n, const RayX& 
   if (!chain_tx<F>(S, n->a, rx, -INFINITY, INFINITY, t1)) return false;
   if (!chain_tx<F>(S, n->a, rx, t1 + kEps, INFINITY, t2)) return false;
   const double rec1tp = gmax(t_min, t1);
-  const double rec2t = gmin(t_max, t2);
+  // tier B (keyed draws): the candidate is computed over the boundary's whole inside and then bounded
+  // like any leaf (newt <= t_max), so it does not depend on the bound in force when the walk gets here
+  const double rec2t = R::kKeyed ? t2 : gmin(t_max, t2);
   if (rec1tp >= rec2t) return false;
   const double rec1t = rec1tp < 0 ? 0 : rec1tp;
   const double ray_length = vlen(r.d);
   const double dist_inside = (rec2t - rec1t) * ray_length;
-  const double rnd = g.draw();
+  double rnd;
+  if constexpr (R::kKeyed) rnd = g.keyed(medium_key(n));
+  else rnd = g.draw();
   const double hit_dist = n->f[0] * m_log<R::kSL>(rnd);
   if (hit_dist > dist_inside) return false;
   const double newt = rec1t + (hit_dist / ray_length);
+  if (R::kKeyed && !(newt <= t_max)) return false;
   h.t = newt;
   h.p = at(r, newt);
   h.n = v3(1, 0, 0);
@@ -745,24 +757,22 @@ __device__ __forceinline__ void trav_restart_ref(Trav& t, int root, double t_max
 }
 
 // A walk that flagged an exact tie at t* = closest is redone as the reference does it, to pick the leaf
-// the reference's order picks among those hit at exactly t*. Its media draws need no repeat: media lie
-// only in the skeleton, which the first walk took in the reference's order under the same bounds (a
-// tie changes which leaf holds the closest t, never its value), so the draws were the reference's. The
-// redo therefore skips media (`lite`) and starts bounded by nextafter(t*): a box test at that bound
-// gives the outcome it gives at any larger bound for every box the ray enters by t*, and what it culls
-// holds no leaf hit at t*; the first leaf hit at t* is accepted as under the reference's larger bound,
-// and from then on the bound is t* itself, as in the reference. A walk whose closest hit is a medium
-// draw (a tie there needs a surface at exactly that random t) is redone in full, its draws rewound.
+// the reference's order picks among those hit at exactly t*. Tier-B media draws are keyed by walk and
+// occurrence (RngPhilox::keyed), so a redo repeats them without rewinding anything. The redo starts
+// bounded by nextafter(t*) (`lite`): a box test at that bound gives the outcome it gives at any larger
+// bound for every box the ray enters by t*, and what it culls holds no leaf hit at t*; the first leaf hit
+// at t* is accepted as under the reference's larger bound, and from then on the bound is t* itself, as in
+// the reference. A walk whose closest hit is a medium's (a tie there needs a surface at exactly that
+// random t) or a rect hit at t = NaN (trav_take) is redone in full.
 // (Kernels for media-free worlds, where ties are rare — C2 none, C3 0.015 per sample — redo in full:
 // the lighter redo's extra state cost the 4-wave spheres kernel 3.5 %.)
-template <unsigned F, class R>
-__device__ __forceinline__ void trav_redo(Trav& t, int root, double t_max, R& g, uint32_t walk_mark) {
+template <unsigned F>
+__device__ __forceinline__ void trav_redo(Trav& t, int root, double t_max) {
   if constexpr (!kRefMixed<F>) {
     trav_restart_ref(t, root, t_max, true);
     return;
   }
-  if (t.best_sub == kSubMedium || t.lite) {  // (a medium's draw, or a NaN-t rect hit (trav_take): in full)
-    g.rewind(walk_mark);
+  if (t.best_sub == kSubMedium || t.lite) {
     trav_restart_ref(t, root, t_max, true);
     return;
   }
@@ -859,7 +869,8 @@ __device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, const rt_node
   const int type = n->type & RT_TYPE_MASK;
   const bool chain = (F & F_INST) && (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE);
   const bool medium = (F & F_MEDIA) && type == RT_NODE_CONSTANT_MEDIUM;  // (always on the skeleton: refsem)
-  if (kRefMixed<F> && medium && t.lite) return;  // (a tie redo picks among surfaces at the tied t: trav_redo)
+  // (a stream-drawn medium's redo picks among surfaces at the tied t: trav_redo; keyed media are tested)
+  if (kRefMixed<F> && !R::kKeyed && medium && t.lite) return;
   if constexpr ((F & F_COUNT) != 0) {
     if (chain || medium) ++cnt.other;
     else ++cnt.prim;
@@ -903,18 +914,28 @@ __device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, const rt_node
     trav_take<F>(S, t, tt, id, chain ? (kSubChain | sub) : sub, side, refsem, p, !chain);
     return;
   }
-  if constexpr ((F & F_MEDIA) != 0) {  // the rest of hit ConstantMedium (Lib.hs:1062-1080)
+  if constexpr ((F & F_MEDIA) != 0) {  // the rest of hit ConstantMedium (Lib.hs:1062-1080; medium_hit)
     const Ray r = plain(t.ray);
     const double rec1tp = gmax(t_min, t1);
-    const double rec2t = gmin(t.closest, tt);
+    const double rec2t = R::kKeyed ? tt : gmin(t.closest, tt);
     if (rec1tp >= rec2t) return;
     const double rec1t = rec1tp < 0 ? 0 : rec1tp;
     const double ray_length = vlen(r.d);
     const double dist_inside = (rec2t - rec1t) * ray_length;
-    const double rnd = g.draw();
+    double rnd;
+    if constexpr (R::kKeyed) rnd = g.keyed(medium_key(n));
+    else rnd = g.draw();
     const double hit_dist = n->f[0] * log_call(rnd);
     if (hit_dist > dist_inside) return;
-    trav_take<F>(S, t, rec1t + (hit_dist / ray_length), id, kSubMedium, side, true, n, false);
+    const double x = rec1t + (hit_dist / ray_length);
+    if constexpr (R::kKeyed) {
+      // bounded like any leaf: accepted at x <= closest (a medium in a re-bounded subtree at exactly
+      // closest is an exact tie, redone in the reference's order)
+      if (!(x <= t.closest)) return;
+      trav_take<F>(S, t, x, id, kSubMedium, side, refsem, n, false);
+    } else {
+      trav_take<F>(S, t, x, id, kSubMedium, side, true, n, false);
+    }
   }
 }
 

@@ -66,9 +66,15 @@ def test_rebuilt_tree_is_a_proper_bvh():
 
 @pytest.mark.parametrize("name", ["cornell_smoke", "cornell", "three_spheres"])
 def test_small_trees_are_not_rebuilt(name):
-    """Worlds whose media-free subtrees all hold < 16 leaves keep the caller's tree."""
+    """Worlds of < 16 leaves keep the caller's tree (media worlds: its unfolded copy, every medium
+    occurrence its own keyed record; the topology is the caller's)."""
     scene, _ = rtamd.make_scene(name, rtamd.randGen(1024))
-    assert rtamd.rebuilt_scene(scene).desc.world_root == scene.desc.world_root
+    assert not rtamd.prepare_scene(scene)["rebuilt_bvh"]
+    rb = rtamd.rebuilt_scene(scene)
+    nodes = rb.nodes
+    if name != "cornell_smoke":
+        assert rb.desc.world_root == scene.desc.world_root
+    assert not np.any(nodes["c"][nodes["type"] == rtamd.RT_NODE_BVH] & rtamd.RT_BVH_ORDERED)
 
 
 def _earth():
@@ -76,68 +82,67 @@ def _earth():
     return np.load(os.path.join(os.path.dirname(__file__), "golden", "earthmap_rgb8.npz"))["rgb"]
 
 
-def test_media_world_keeps_its_skeleton():
-    """next_week_final (two ConstantMedium, a Translate/Rotate frame over 1000 spheres): the BVH
-    nodes above the media keep their boxes, children order and left-first semantics (no
-    RT_BVH_ORDERED); everything below an ORDERED node is media-free; the media nodes themselves and
-    every leaf are the caller's records (same ids); the frame's inner tree is re-bounded too."""
-    scene, _ = rtamd.make_scene("next_week_final", rtamd.randGen(1024), earth=_earth())
+def _medium_occurrences(nodes, i, out):
+    """The medium records reached from node i in the walk's preorder (BVH left first, into frames)."""
+    nd = nodes[i]
+    t = int(nd["type"])
+    if t == rtamd.RT_NODE_CONSTANT_MEDIUM:
+        out.append(i)
+    elif t == rtamd.RT_NODE_BVH:
+        _medium_occurrences(nodes, int(nd["a"]), out)
+        _medium_occurrences(nodes, int(nd["b"]), out)
+    elif t in (rtamd.RT_NODE_TRANSLATE, rtamd.RT_NODE_ROTATE):
+        _medium_occurrences(nodes, int(nd["a"]), out)
+    return out
+
+
+@pytest.mark.parametrize("name", ["next_week_final", "cornell_smoke"])
+def test_media_are_unfolded_and_keyed(name):
+    """rt_rebuild_bvh (the upload's tree): the caller's records untouched (appended only); every medium
+    occurrence of the caller's tree — preorder, BVH left first, BVHNode h h and shared sub-trees counted
+    once per path — is its own record with f[1] = its preorder rank + 1 (the tier-B draw key); the
+    device's tree reaches exactly those keyed records, each once; the same medium records (boundary,
+    density, phase material)."""
+    scene, _ = rtamd.make_scene(name, rtamd.randGen(1024), earth=_earth() if name == "next_week_final" else None)
     rb = rtamd.rebuilt_scene(scene)
     old, new = scene.nodes, rb.nodes
     n0 = scene.desc.n_nodes
-    assert rb.desc.world_root != scene.desc.world_root and rb.desc.n_nodes > n0
-    assert np.array_equal(new[:n0], old)  # the caller's records are untouched (appended only)
+    assert np.array_equal(new[:n0], old)
+    ref = _medium_occurrences(old, scene.desc.world_root, [])
+    dev = _medium_occurrences(new, rb.desc.world_root, [])
+    assert len(ref) >= 2 and len(dev) == len(ref)
+    keys = sorted(int(new[i]["f"][1]) for i in dev)
+    assert keys == list(range(1, len(ref) + 1)) and len(set(dev)) == len(dev)
+    by_key = {int(new[i]["f"][1]): i for i in dev}
+    for rank, i in enumerate(ref):
+        j = by_key[rank + 1]
+        assert (new[j]["f"][0] == old[i]["f"][0] and new[j]["a"] == old[i]["a"] and new[j]["b"] == old[i]["b"])
 
-    def has_media(nodes, i):
-        t = int(nodes[i]["type"])
-        if t == rtamd.RT_NODE_CONSTANT_MEDIUM:
-            return True
-        if t == rtamd.RT_NODE_BVH:
-            return has_media(nodes, int(nodes[i]["a"])) or has_media(nodes, int(nodes[i]["b"]))
-        if t in (rtamd.RT_NODE_TRANSLATE, rtamd.RT_NODE_ROTATE):
-            return has_media(nodes, int(nodes[i]["a"]))
-        return False
 
-    def media_ids(nodes, i, out):
-        nd = nodes[i]
-        t = int(nd["type"])
-        if t == rtamd.RT_NODE_CONSTANT_MEDIUM:
-            out.append(i)
-        elif t == rtamd.RT_NODE_BVH:
-            media_ids(nodes, int(nd["a"]), out)
-            media_ids(nodes, int(nd["b"]), out)
-        elif t in (rtamd.RT_NODE_TRANSLATE, rtamd.RT_NODE_ROTATE):
-            media_ids(nodes, int(nd["a"]), out)
-        return out
-
-    ordered_frames = 0
-
-    def check(i, below_ordered):
-        nonlocal ordered_frames
-        nd = new[i]
-        t = int(nd["type"])
-        if t == rtamd.RT_NODE_BVH:
-            ordered = (int(nd["c"]) & rtamd.RT_BVH_ORDERED) != 0
-            if has_media(new, i):
-                assert not ordered and not below_ordered  # skeleton
-            if ordered and i >= n0:
-                assert not has_media(new, i)
-            check(int(nd["a"]), below_ordered or ordered)
-            check(int(nd["b"]), below_ordered or ordered)
-        elif t in (rtamd.RT_NODE_TRANSLATE, rtamd.RT_NODE_ROTATE):
-            inner = int(new[int(nd["a"])]["c"]) if int(new[int(nd["a"])]["type"]) == rtamd.RT_NODE_BVH else 0
-            ordered_frames += (inner & rtamd.RT_BVH_ORDERED) != 0
-            check(int(nd["a"]), below_ordered)
-    check(rb.desc.world_root, False)
-    assert ordered_frames >= 1
-    assert media_ids(new, rb.desc.world_root, []) == media_ids(old, scene.desc.world_root, [])
+def test_media_world_is_rebuilt_whole():
+    """next_week_final (two ConstantMedium, a Translate/Rotate frame over 1000 spheres): with keyed
+    media the world keeps no skeleton above them — its root is an SAH (RT_BVH_ORDERED) node over every
+    leaf, media included, and the frame's inner tree is re-bounded too; the mixed walk then takes one
+    4-wide tree from the root (rt_prepare_scene: mixed_wide)."""
+    scene, _ = rtamd.make_scene("next_week_final", rtamd.randGen(1024), earth=_earth())
+    rb = rtamd.rebuilt_scene(scene)
+    nodes = rb.nodes
+    root = rb.desc.world_root
+    assert nodes[root]["type"] == rtamd.RT_NODE_BVH and nodes[root]["c"] & rtamd.RT_BVH_ORDERED
+    frames = [i for i in range(len(nodes)) if nodes[i]["type"] == rtamd.RT_NODE_TRANSLATE and i >= scene.desc.n_nodes]
+    assert frames  # the 1000-sphere frame copied with its inner tree re-bounded
+    inner = nodes[int(nodes[int(nodes[frames[-1]]["a"])]["a"])]
+    assert inner["type"] == rtamd.RT_NODE_BVH and inner["c"] & rtamd.RT_BVH_ORDERED
+    info = rtamd.prepare_scene(scene)
+    assert info["rebuilt_bvh"] and info["mixed_wide"] and info["n_wide_nodes"] > 300
 
 
 @pytest.mark.parametrize("name", ["next_week_final", "cornell_smoke"])
 def test_skeleton_gives_the_references_closest_hits_and_draws(name):
-    """The oracle (the reference's own hit recursion, media draws included) over the device's tree
-    and over the caller's tree: every closest hit identical, including medium hits, whose draw
-    depends on the bound the walk carries when it reaches the medium."""
+    """The oracle's hit recursion (tier-B semantics: keyed medium draws, unbounded medium candidates)
+    over the device's tree and over the caller's tree: every closest hit identical, medium hits
+    included — the keys follow the occurrences (f[1] on the device's records, preorder ranks on the
+    caller's), not the order the walk reaches them in."""
     scene, _ = rtamd.make_scene(name, rtamd.randGen(1024), earth=_earth() if name == "next_week_final" else None)
     rb = rtamd.rebuilt_scene(scene)
     rng = np.random.default_rng(11)
