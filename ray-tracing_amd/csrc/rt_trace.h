@@ -1325,7 +1325,7 @@ __device__ __forceinline__ bool trav_finish(const Scene& S, const Trav& t, const
     h.u = 0;
     h.v = 0;
     h.ff = 1;
-    h.mat = S.nodes[t.best_node].b;
+    h.mat = n->b;  // (n: the leaf-table copy for a 4-wide walk's slot, whose id carries kSlotTag)
   }
   if constexpr ((F & F_INST) != 0) {
     if (!med && (sub & kSubChain)) {

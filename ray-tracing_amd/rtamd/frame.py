@@ -51,41 +51,65 @@ class ShardedFrame:
 
     # ------------------------------------------------------------------ one step
     def step(self, kernel_ms: Optional[Callable[[], float]] = None):
-        """Render this rank's slab, gather the slabs, assemble on rank 0 (stream-ordered on the GPU)."""
+        """Render this rank's slab, gather the slabs, assemble on rank 0 (stream-ordered on the GPU).
+
+        Timings per step (finish()): GPU events after the render, after the collective, after the
+        host-staged copy back to the device (gloo only) and after the assembly; and host wall-clock
+        marks around the same phases, which add up to the step's wall time. (In a rehearsal whose
+        ranks share one GPU the GPU intervals also hold the other ranks' kernels: e.g. rank 0's
+        assembly queues behind rank 1's next render.)"""
+        import time
         torch = self.torch
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if self.cuda else None
+        h = [time.perf_counter()]
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if self.cuda else None
         self._render(self.p, self.slab)
         if ev:
             ev[0].record()
+        h.append(time.perf_counter())
         if self.gather:
             import torch.distributed as dist
             if self.backend == "nccl":
                 dist.all_gather_into_tensor(self.slabs, self.slab)  # RCCL over xGMI
+                if ev:
+                    ev[1].record()
             else:
-                host = self.slab.cpu()
+                host = self.slab.cpu()  # (waits for this rank's render)
                 parts = [torch.empty_like(host) for _ in range(self.world)]
                 dist.all_gather(parts, host)
-                self.slabs.copy_(torch.stack(parts))
+                if ev:
+                    ev[1].record()
+                self.slabs.copy_(torch.stack(parts))  # the host-staged copy back to the device
             src = self.slabs
         else:
             src = self.slab
+            if ev:
+                ev[1].record()
         if ev:
-            ev[1].record()
+            ev[2].record()
+        h.append(time.perf_counter())
         if self.rank == 0:
             self._assemble(self.p, src, self.image)
         if ev:
-            ev[2].record()
-        self._ev.append((ev, kernel_ms() if kernel_ms else None))
+            ev[3].record()
+        h.append(time.perf_counter())
+        self._ev.append((ev, kernel_ms() if kernel_ms else None, h))
 
     def finish(self) -> List[dict]:
         """Per-step timings (call after a device synchronize): render kernel ms (HIP events around
-        the launch, from kernel_ms), all-gather ms and assemble ms (events on the current stream)."""
+        the launch, from kernel_ms), all-gather, host-staged copy and assemble ms (events on the current
+        stream), and the host wall-clock split of the step (host_*_ms)."""
         out = []
-        for ev, kms in self._ev:
+        for ev, kms, h in self._ev:
             t = {"kernel_ms": kms}
             if ev:
                 t["gather_ms"] = ev[0].elapsed_time(ev[1])
-                t["assemble_ms"] = ev[1].elapsed_time(ev[2])
+                t["h2d_ms"] = ev[1].elapsed_time(ev[2])  # (gloo's host-staged copy; 0 with nccl)
+                t["assemble_ms"] = ev[2].elapsed_time(ev[3])
+            # host wall clock: enqueueing the render, the gather (gloo: waiting for the render, the
+            # collective and the copy back), enqueueing the assembly
+            t["host_render_ms"] = (h[1] - h[0]) * 1e3
+            t["host_gather_ms"] = (h[2] - h[1]) * 1e3
+            t["host_assemble_ms"] = (h[3] - h[2]) * 1e3
             out.append(t)
         self._ev.clear()
         self.timings.extend(out)
@@ -93,8 +117,8 @@ class ShardedFrame:
 
     def summary(self) -> dict:
         """Mean of each timing over the recorded steps."""
-        keys = [k for k in ("kernel_ms", "gather_ms", "assemble_ms") if self.timings and
-                self.timings[0].get(k) is not None]
+        keys = [k for k in ("kernel_ms", "gather_ms", "h2d_ms", "assemble_ms", "host_render_ms", "host_gather_ms",
+                            "host_assemble_ms") if self.timings and self.timings[0].get(k) is not None]
         return {k: float(np.mean([t[k] for t in self.timings])) for k in keys}
 
 
