@@ -409,8 +409,11 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     }
     // ---- shade finished walks, then set up the next walk for every lane that is not walking
     // exact tie, or a NaN-t rect hit in a re-bounded subtree (trav_take: `lite` in a first walk): redo
-    // this walk as the reference does (once)
-    if (ready && (t.tie || t.lite) && !t.redo) {
+    // this walk as the reference does (once) — unless the path's throughput is NaN in every channel
+    // already: its colour is NaN whichever leaf the reference's order picks (NaN * anything, including
+    // the background's 0, is NaN), and a tier-B sample's draws reach no other sample. (NaN-t hits come
+    // from the Lambertian quirk's +x ray in a box top's plane, whose pdf is 0 / 0: DESIGN.md §4.3.)
+    if (ready && (t.tie || t.lite) && !t.redo && !(thr.x != thr.x && thr.y != thr.y && thr.z != thr.z)) {
       ready = false;
       if constexpr ((F & F_COUNT) != 0) ++cnt.ties;
       trav_redo<F>(t, S.world_ref, INFINITY);

@@ -203,7 +203,9 @@ def test_coplanar_ties(gpu_ctx, kind):
     assert info["rebuilt_bvh"], info
     gpu_ctx.upload(sc)
     cam = rtamd.newCamera((0.3, 0.1, 4.0), (0.2, 0.0, 0.0), (0.0, 1.0, 0.0), 35.0, 1.0, 0.0, 4.0, 0.0, 1.0)
-    p = rtamd.make_params(64, 64, 4, 10, rtamd.RT_RNG_PHILOX, seed=13)
+    # (depth 1: camera rays only — the Lambertian quirk's +x rays, with lights Unhittable, run in the
+    # rects' plane and end on NaN-t hits, redone for their own reason, trav_take)
+    p = rtamd.make_params(64, 64, 4, 1, rtamd.RT_RNG_PHILOX, seed=13)
     redos = gpu_ctx.render_work(cam, p)["tie_redos"]
     rgb_g, lin_g, _ = gpu_ctx.render(cam, p, linear=True)
     rgb_o, lin_o, _, _ = pyoracle.render(sc, cam, p)
@@ -213,4 +215,4 @@ def test_coplanar_ties(gpu_ctx, kind):
     if kind == "same":
         assert redos == 0
     else:
-        assert redos > 100  # (the camera rays through the overlap, and more)
+        assert redos > 100  # (the camera rays through the overlap)
