@@ -413,7 +413,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     // already: its colour is NaN whichever leaf the reference's order picks (NaN * anything, including
     // the background's 0, is NaN), and a tier-B sample's draws reach no other sample. (NaN-t hits come
     // from the Lambertian quirk's +x ray in a box top's plane, whose pdf is 0 / 0: DESIGN.md §4.3.)
-    if (ready && (t.tie || t.lite) && !t.redo && !(thr.x != thr.x && thr.y != thr.y && thr.z != thr.z)) {
+    if (ready && (t.tie || (kRefMixed<F> && t.lite)) && !t.redo && !(thr.x != thr.x && thr.y != thr.y && thr.z != thr.z)) {
       ready = false;
       if constexpr ((F & F_COUNT) != 0) ++cnt.ties;
       trav_redo<F>(t, S.world_ref, INFINITY);
@@ -731,7 +731,7 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
     if (S.ref_walk) trav_restart_ref(t, S.world, tmax);  // (the re-bounded skeleton, mixed walk)
     bool walking = true;
     walk_until<F>(S, t, walking, tmin, stk, RT_BLOCK, joint != 0, 0, 0, cnt, g, side);
-    if (t.tie || t.lite) {
+    if (t.tie || (kRefMixed<F> && t.lite)) {
       trav_redo<F>(t, S.world_ref, tmax);
       while (trav_step<F>(S, t, tmin, stk, RT_BLOCK, joint != 0, cnt, g, side)) {
       }

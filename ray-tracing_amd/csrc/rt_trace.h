@@ -825,10 +825,20 @@ __device__ __forceinline__ bool tie_same(const Scene& S, const Trav& t, const rt
 template <unsigned F>
 __device__ __forceinline__ void trav_take(const Scene& S, Trav& t, double x, int id, int sub, Side& side, bool refsem,
                                           const rt_node* leaf, bool plain) {
-  if (refsem || x < t.closest) {
+  // A rect hit at t = NaN (a ray in the plane of a face it runs along — the Lambertian quirk's +x ray
+  // from a point exactly on a box top: rectHit rejects only t < tmin or t > tmax, Lib.hs:1014-1015) is
+  // taken like a closer hit, as the reference takes it; the reference keeps it, or replaces it, by its
+  // own tree order (every later test against a NaN bound: boxes fail, rects pass). The walk ends here
+  // (closest_up(NaN) is 2^-1074, tmax32 0) and is flagged for a full redo in the reference's order
+  // (trav_redo): by `tie`, and in walks that mix reference-semantics leaves (kRefMixed), whose later
+  // replacement of the NaN clears `tie`, by `lite` too. (No branch
+  // of its own: as one, never taken, it cost the Cornell kernel 3 %.)
+  const bool nan_t = (F & F_RECT) != 0 && x != x;
+  if (refsem || x < t.closest || nan_t) {
     // (a tie at the old closest no longer matters: only leaves hit at the final closest t compete, and
     // the bound the walk carried on with was the same whichever tied leaf won)
-    t.tie = false;
+    t.tie = nan_t;
+    if constexpr ((F & F_RECT) != 0 && kRefMixed<F>) t.lite = t.lite | nan_t;
     t.closest = x;
     t.best_node = id;
     t.best_sub = sub;
@@ -836,24 +846,10 @@ __device__ __forceinline__ void trav_take(const Scene& S, Trav& t, double x, int
       t.best_level = t.level;
       for (int k = 0; k < t.level; ++k) side.best(k) = side.frame(k);
     }
-    if constexpr (kRay32<F>) t.tmax32 = f32_upper(x);
+    if constexpr (kRay32<F>) t.tmax32 = nan_t ? 0.0f : f32_upper(x);
   } else if (x == t.closest && id != t.best_node) {  // (the same leaf twice is no tie)
     // (a tie whose records shade identically needs no redo: tie_same)
     if (!tie_same<F>(S, t, leaf, sub, plain)) t.tie = true;
-  } else if constexpr ((F & F_RECT) != 0) {
-    // A rect hit at t = NaN (a ray in the plane of a face it runs along — the Lambertian quirk's +x ray
-    // from a point exactly on a box top: rectHit rejects only t < tmin or t > tmax, Lib.hs:1014-1015).
-    // The reference keeps it as its closest hit, or replaces it, by its own tree order (every later test
-    // against a NaN bound: boxes fail, rects pass): the walk ends here (closest_up(NaN) bounds it to
-    // 2^-1074) and is redone in full in the reference's order (trav_redo).
-    // (`lite` is a redo's flag, false in a first walk: here it marks the NaN hit for trav_redo and stays
-    // set when a reference-semantics leaf later replaces the NaN and clears `tie`)
-    if (x != x) {
-      t.closest = x;
-      t.tie = true;
-      t.lite = true;
-      if constexpr (kRay32<F>) t.tmax32 = 0.0f;
-    }
   }
 }
 // A leaf: a primitive, an instance chain ending in one (its t and face only: the record is built once,
