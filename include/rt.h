@@ -76,6 +76,10 @@ enum rt_node_type {
  * device-side rebuild carry 0x40000000 | split axis instead; they never occur in a lights tree.)
  */
 #define RT_BVH_ORDERED 0x40000000 /* rebuilt world BVH node: c = this flag | split axis */
+#define RT_BVH_MEDIA_FIRST 0x10000000 /* with RT_BVH_ORDERED: a rebuilt world's top node whose left child
+                                         is a medium occurrence (not inside an instance frame), entered
+                                         before the right child (the rest of the world) whatever the ray
+                                         direction: its candidate bounds the walk from the start */
 
 typedef struct rt_node {
     double f[6];

@@ -373,6 +373,7 @@ int rebuild_world_bvh(std::vector<rt_node>& nodes, int root) {
 namespace {
 
 bool kMediaSkeleton = false;  // (RTAMD_MEDIA_SKELETON=1, read by rebuild_media_skeleton)
+bool kMediaFirst = true;      // (RTAMD_MEDIA_FIRST=0 leaves the world's media in its SAH tree)
 
 // rebuild_media_skeleton's recursion: the id that replaces node `id` (itself when unchanged).
 int skeleton(std::vector<rt_node>& nodes, int id, int depth) {
@@ -386,6 +387,19 @@ int skeleton(std::vector<rt_node>& nodes, int id, int depth) {
       std::vector<int> leaves;
       std::vector<char> seen(nodes.size(), 0);
       collect_leaves(nodes, id, leaves, seen);
+      // The world's own media (outside instance frames) are hoisted out of the SAH tree: a chain of
+      // RT_BVH_MEDIA_FIRST nodes above it, one per medium, entered left (the medium) first. A medium's
+      // tier-B candidate does not depend on the walk's bound or order (keyed draw, unbounded candidate), so
+      // testing it first changes no result, and its candidate (the fog of next_week_final is hit by
+      // nearly every ray) bounds the walk of the rest from the start; the rest's tree is no longer
+      // inflated by a medium's box (the fog's boundary is a radius-5000 sphere around the whole scene).
+      std::vector<int> media;
+      if (depth == 0 && kMediaFirst) {
+        std::vector<int> rest;
+        for (int leaf : leaves) (nodes[leaf].type == RT_NODE_CONSTANT_MEDIUM ? media : rest).push_back(leaf);
+        if (!rest.empty() && !media.empty()) leaves.swap(rest);
+        else media.clear();
+      }
       bool changed = false;
       for (int& leaf : leaves) {
         if (nodes[leaf].type == RT_NODE_UNHITTABLE || nodes[leaf].type == RT_NODE_EXT) return id;
@@ -393,9 +407,26 @@ int skeleton(std::vector<rt_node>& nodes, int id, int depth) {
         changed |= nl != leaf;
         leaf = nl;
       }
-      if (leaves.size() < 16 && !changed) return id;
-      const int r = sah_over_leaves(nodes, leaves);
-      return r < 0 ? id : r;
+      // (small worlds keep the caller's tree, media where they are)
+      if (leaves.size() + media.size() < 16 && !changed) return id;
+      int r = leaves.size() == 1 ? leaves[0] : sah_over_leaves(nodes, leaves);
+      if (r < 0) return id;
+      for (size_t k = media.size(); k-- > 0;) {
+        Box mb, rb;
+        if (!flat_box(nodes, media[k], &mb) || !flat_box(nodes, r, &rb)) return id;
+        rt_node h{};
+        for (int i = 0; i < 3; ++i) {
+          h.f[i] = std::min(mb.mn[i], rb.mn[i]);
+          h.f[3 + i] = std::max(mb.mx[i], rb.mx[i]);
+        }
+        h.type = RT_NODE_BVH;
+        h.a = media[k];
+        h.b = r;
+        h.c = RT_BVH_ORDERED | RT_BVH_MEDIA_FIRST;
+        nodes.push_back(h);
+        r = (int)nodes.size() - 1;
+      }
+      return r;
     }
     const int a = skeleton(nodes, n.a, depth + 1), b = skeleton(nodes, n.b, depth + 1);
     if (a == n.a && b == n.b) return id;
@@ -427,6 +458,8 @@ int skeleton(std::vector<rt_node>& nodes, int id, int depth) {
 int rebuild_media_skeleton(std::vector<rt_node>& nodes, int root) {
   const char* ms = std::getenv("RTAMD_MEDIA_SKELETON");
   kMediaSkeleton = ms && ms[0] == '1';
+  const char* mf = std::getenv("RTAMD_MEDIA_FIRST");
+  kMediaFirst = !(mf && mf[0] == '0');
   const size_t n0 = nodes.size();
   const int r = skeleton(nodes, root, 0);
   std::vector<int> need;

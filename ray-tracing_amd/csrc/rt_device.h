@@ -265,8 +265,10 @@ struct RngPhilox {
   // unfold_media). A walk consumes no stream words, so the counter names the walk (the path's position in
   // its stream) and the key the occurrence: the draw does not depend on the order media are visited in.
   // Word 3 >= 2^31 keeps these blocks apart from the stream's (word 3 = 0).
-  __device__ __forceinline__ double keyed(uint32_t key) const {
-    uint32_t c[4] = {consumed(), sample, pid, 0x80000000u | key};
+  __device__ __forceinline__ double keyed(uint32_t key) const { return keyed_at(k0, k1, consumed(), sample, pid, key); }
+  static __device__ __forceinline__ double keyed_at(uint32_t k0, uint32_t k1, uint32_t walk, uint32_t sample,
+                                                    uint32_t pid, uint32_t key) {
+    uint32_t c[4] = {walk, sample, pid, 0x80000000u | key};
     philox(c, k0, k1);
     return word_to_draw((uint64_t)c[0] | ((uint64_t)c[1] << 32));
   }

@@ -51,7 +51,8 @@ struct Box {
 // while a is walked (hit BVHNode, src/Lib.hs:971-988). A rebuilt node (RT_BVH_ORDERED) enters the
 // child on the ray's side of the split first, so either child can be walked above the other.
 inline int bvh_stack_need(const rt_node& x, int need_a, int need_b) {
-  if (x.c & RT_BVH_ORDERED) return 1 + (need_a > need_b ? need_a : need_b);
+  // (either child first; an RT_BVH_MEDIA_FIRST node enters its left child first, like a reference node)
+  if ((x.c & RT_BVH_ORDERED) && !(x.c & RT_BVH_MEDIA_FIRST)) return 1 + (need_a > need_b ? need_a : need_b);
   return (1 + need_a > need_b) ? 1 + need_a : need_b;
 }
 

@@ -521,6 +521,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
       trav_begin<F>(t, plain(t.ray), S.world, kEps, INFINITY);
       // worlds with media or frames: the reference's order over the re-bounded skeleton
       if (S.ref_walk) trav_restart_ref(t, S.world, INFINITY);
+      trav_media_first<F>(S, t, kEps, cnt, g, side);  // (hoisted media: RT_BVH_MEDIA_FIRST)
       walking = true;
     }
     if (!walking) break;  // this lane is finished; the rest of the wave carries on without it

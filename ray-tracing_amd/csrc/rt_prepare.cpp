@@ -54,9 +54,10 @@ struct Validator {
         case RT_NODE_BVH:
           if (!child_ok(i, x.a) || !child_ok(i, x.b)) return fail("BVH child must precede its parent");
           if (x.c <= 0) return fail("BVH size must be positive");
-          // an ordered (rebuilt) node's c is exactly the flag and its split axis: the walks read other
-          // bits of c as internal tags (RT_WROOT and a wide root index, set only by the upload)
-          if ((x.c & RT_BVH_ORDERED) && (x.c & ~RT_BVH_ORDERED) > 2)
+          // an ordered (rebuilt) node's c is exactly the flag, RT_BVH_MEDIA_FIRST or not, and its split axis:
+          // the walks read other bits of c as internal tags (RT_WROOT and a wide root index, set only by
+          // the upload)
+          if ((x.c & RT_BVH_ORDERED) && (x.c & ~(RT_BVH_ORDERED | RT_BVH_MEDIA_FIRST)) > 2)
             return fail("RT_BVH_ORDERED node must carry only its split axis (0..2) in c");
           stack_need[i] = rt::bvh_stack_need(x, stack_need[x.a], stack_need[x.b]);
           frame_depth[i] = std::max(frame_depth[x.a], frame_depth[x.b]);
@@ -192,6 +193,10 @@ void mixed_wide_trees(PreparedScene& P, const std::vector<rt_node>& host, const 
     const int ty = x.type & RT_TYPE_MASK;
     if (ty == RT_NODE_BVH) {
       const bool ord = (x.c & RT_BVH_ORDERED) != 0;
+      if (ord && (x.c & RT_BVH_MEDIA_FIRST)) {  // a hoisted medium (rt_bvh.cpp skeleton): in no 4-wide tree
+        find(x.b, lvl);
+        return;
+      }
       int next = lvl;
       if (ord && lvl < kIn) {
         const int here = lvl < 0 ? 0 : lvl;
@@ -266,7 +271,7 @@ void mixed_wide_trees(PreparedScene& P, const std::vector<rt_node>& host, const 
     int r = 0;
     if (ty == RT_NODE_BVH) {
       if (wroot[id] >= 0) r = wneed(wroot[id]);
-      else if (x.c & RT_BVH_ORDERED) r = 1 + std::max(need_of(x.a), need_of(x.b));
+      else if ((x.c & RT_BVH_ORDERED) && !(x.c & RT_BVH_MEDIA_FIRST)) r = 1 + std::max(need_of(x.a), need_of(x.b));
       else r = std::max(1 + need_of(x.a), need_of(x.b));
     } else if ((ty == RT_NODE_TRANSLATE || ty == RT_NODE_ROTATE) && !(x.type & RT_CHAIN_PRIM)) {
       r = 1 + need_of(x.a);

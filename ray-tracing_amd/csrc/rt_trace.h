@@ -485,7 +485,7 @@ __device__ __forceinline__ bool traverse(const Scene& S, int root, const Ray& wr
         // Rebuilt (media-free) trees: visit the child on the ray's side of the split first;
         // the closest hit is order-independent there. Reference trees stay left-first.
         const int c = n->c;
-        const bool flip = (c & RT_BVH_ORDERED) && comp(ray.d, c & 3) < 0;
+        const bool flip = (c & RT_BVH_ORDERED) && !(c & RT_BVH_MEDIA_FIRST) && comp(ray.d, c & 3) < 0;
         stk[(sp++) * stride] = flip ? n->a : n->b;
         node = flip ? n->b : n->a;
         continue;
@@ -852,6 +852,49 @@ __device__ __forceinline__ void trav_take(const Scene& S, Trav& t, double x, int
     if (!tie_same<F>(S, t, leaf, sub, plain)) t.tie = true;
   }
 }
+// A hoisted medium's tier-B candidate (RT_BVH_MEDIA_FIRST, rt_bvh.cpp): exactly the walk's medium leaf
+// (trav_leaf: boundary queries over (-inf, inf) and (t1 + eps, inf), the keyed draw, OCML's log), or -1
+// when the ray draws no hit in it (a candidate is >= t_min > 0). Not inlined: it runs where lanes start
+// their walks, and inlined it would be a second copy of the primitive tests in the render loop.
+template <unsigned F>
+__device__ __forceinline__ double hoisted_medium_t(const rt_node* nodes, int id, RayX rx, double t_min, uint32_t k0,
+                                                uint32_t k1, uint32_t walk, uint32_t sample, uint32_t pid) {
+  Scene S{};
+  S.nodes = nodes;
+  const rt_node* n = &nodes[id];
+  double t1, t2;
+  if (!chain_tx<F>(S, n->a, rx, -INFINITY, INFINITY, t1)) return -1.0;
+  if (!chain_tx<F>(S, n->a, rx, t1 + kEps, INFINITY, t2)) return -1.0;
+  const double rec1tp = gmax(t_min, t1);
+  if (rec1tp >= t2) return -1.0;
+  const double rec1t = rec1tp < 0 ? 0 : rec1tp;
+  const double ray_length = vlen(rx.d);
+  const double dist_inside = (t2 - rec1t) * ray_length;
+  const double rnd = RngPhilox::keyed_at(k0, k1, walk, sample, pid, medium_key(n));
+  const double hit_dist = n->f[0] * log(rnd);
+  if (hit_dist > dist_inside) return -1.0;
+  return rec1t + (hit_dist / ray_length);
+}
+// The walk's prelude (tier B, worlds with hoisted media): the RT_BVH_MEDIA_FIRST chain at the top of the
+// world is taken here, each medium's candidate offered to trav_take like a leaf of a re-bounded subtree,
+// without the chain's box tests (they only cull; the medium tests are exact), so that the walk starts at
+// the rest of the world already bounded by the media. Lanes run it where they start walks together.
+template <unsigned F, class R>
+__device__ __forceinline__ void trav_media_first(const Scene& S, Trav& t, double t_min, Cnt& cnt, const R& g,
+                                                 Side& side) {
+  if constexpr ((F & F_MEDIA) != 0 && R::kKeyed) {
+    for (;;) {
+      if (!(t.node >= 0 && (t.node & (RT_WNODE | RT_IDTAGS)) == RT_ISBOX)) return;
+      const rt_node* n = &S.nodes[t.node & ~(RT_SUB | RT_IDTAGS)];
+      if (!(n->c & RT_BVH_MEDIA_FIRST)) return;
+      const int m = n->a & ~RT_IDTAGS;
+      if constexpr ((F & F_COUNT) != 0) ++cnt.other;
+      const double x = hoisted_medium_t<F>(S.nodes, m, t.ray, t_min, g.k0, g.k1, g.consumed(), g.sample, g.pid);
+      if (x >= 0.0 && x <= t.closest) trav_take<F>(S, t, x, m, kSubMedium, side, false, &S.nodes[m], false);
+      t.node = n->b | RT_SUB;  // (the rest: below an ordered node, a re-bounded subtree)
+    }
+  }
+}
 // A leaf: a primitive, an instance chain ending in one (its t and face only: the record is built once,
 // in trav_finish), or a ConstantMedium (ref walks only: its one draw happens here, in the reference's
 // order and under its bound, Lib.hs:1053-1080). The three kinds share ONE inlined primitive test
@@ -1103,7 +1146,7 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
           break;
         }
       }
-      const bool flip = ord && comp(t.ray.d, c & 3) < 0;
+      const bool flip = ord && !(c & RT_BVH_MEDIA_FIRST) && comp(t.ray.d, c & 3) < 0;  // (hoisted media first)
       const int ctag = (kRefMixed<F> && ord) ? RT_SUB : tag;
       stk[(t.sp++) * stride] = (flip ? n->a : n->b) | ctag;
       t.node = (flip ? n->b : n->a) | ctag;

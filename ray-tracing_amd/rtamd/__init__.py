@@ -37,6 +37,7 @@ RT_UPLOAD_REFERENCE_BVH = 1
 RT_DEBUG_RESUMABLE = 4  # rt_debug_closest_hits: the render loop's resumable binary walk
 RT_DEBUG_WIDE = 8       # rt_debug_closest_hits: the resumable walk over the 4-wide fp32-box tree
 RT_BVH_ORDERED = 0x40000000
+RT_BVH_MEDIA_FIRST = 0x10000000
 MATH_OPS = {"div": 0, "div_exact": 1, "sqrt": 2, "sin": 3, "cos": 4, "atan": 5, "asin": 6, "log": 7, "pow": 8,
             "ghc_atan2": 9, "tan": 10, "pow5": 11, "sl_sin": 12, "sl_cos": 13, "sl_atan": 14, "sl_asin": 15,
             "sl_log": 16, "sl_ghc_atan2": 17}  # sl_*: include/rt_libm.h (RT_FLAG_SHARED_LIBM)

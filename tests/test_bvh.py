@@ -121,14 +121,23 @@ def test_media_are_unfolded_and_keyed(name):
 
 def test_media_world_is_rebuilt_whole():
     """next_week_final (two ConstantMedium, a Translate/Rotate frame over 1000 spheres): with keyed
-    media the world keeps no skeleton above them — its root is an SAH (RT_BVH_ORDERED) node over every
-    leaf, media included, and the frame's inner tree is re-bounded too; the mixed walk then takes one
-    4-wide tree from the root (rt_prepare_scene: mixed_wide)."""
+    media the world keeps no skeleton above them — its two media are hoisted into a chain of
+    RT_BVH_MEDIA_FIRST nodes (medium left, the rest right), below which an SAH (RT_BVH_ORDERED) tree
+    spans every other leaf, and the frame's inner tree is re-bounded too; the mixed walk then takes one
+    4-wide tree below the chain (rt_prepare_scene: mixed_wide)."""
     scene, _ = rtamd.make_scene("next_week_final", rtamd.randGen(1024), earth=_earth())
     rb = rtamd.rebuilt_scene(scene)
     nodes = rb.nodes
     root = rb.desc.world_root
+    media = []
+    while nodes[root]["type"] == rtamd.RT_NODE_BVH and nodes[root]["c"] & rtamd.RT_BVH_MEDIA_FIRST:
+        assert nodes[root]["c"] & rtamd.RT_BVH_ORDERED
+        media.append(int(nodes[root]["a"]))
+        root = int(nodes[root]["b"])
+    assert len(media) == 2 and all(nodes[m]["type"] == rtamd.RT_NODE_CONSTANT_MEDIUM for m in media)
+    assert sorted(int(nodes[m]["f"][1]) for m in media) == [1, 2]  # (keyed occurrences)
     assert nodes[root]["type"] == rtamd.RT_NODE_BVH and nodes[root]["c"] & rtamd.RT_BVH_ORDERED
+    assert not (nodes[root]["c"] & rtamd.RT_BVH_MEDIA_FIRST)
     frames = [i for i in range(len(nodes)) if nodes[i]["type"] == rtamd.RT_NODE_TRANSLATE and i >= scene.desc.n_nodes]
     assert frames  # the 1000-sphere frame copied with its inner tree re-bounded
     inner = nodes[int(nodes[int(nodes[frames[-1]]["a"])]["a"])]
@@ -238,7 +247,7 @@ def _walk_need(nodes, node, signs, memo):
     t = int(nd["type"])
     if t == rtamd.RT_NODE_BVH:
         c = int(nd["c"])
-        flip = (c & rtamd.RT_BVH_ORDERED) != 0 and signs[c & 3] < 0
+        flip = (c & rtamd.RT_BVH_ORDERED) != 0 and not (c & rtamd.RT_BVH_MEDIA_FIRST) and signs[c & 3] < 0
         first, second = (int(nd["b"]), int(nd["a"])) if flip else (int(nd["a"]), int(nd["b"]))
         r = max(1 + _walk_need(nodes, first, signs, memo), _walk_need(nodes, second, signs, memo))
     elif t in (rtamd.RT_NODE_TRANSLATE, rtamd.RT_NODE_ROTATE):
