@@ -364,14 +364,17 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   // vs 219.7 at 0 and 232 without postponement; C5 (16 spp) 219.9 ms at 16/64 vs 326 at 0)
   A.leaf_stop = leaf_env ? std::max(0, std::min(64, std::atoi(leaf_env))) : A.trav_stop;
   // binary walks of the full variant (media / frame worlds, C4): box-only steps while more than
-  // box_first/64 of the live lanes are at BVH nodes (measured on C4 at 100 spp: 64 (never) 430 ms,
-  // 48 416, 32 406, 16 398, 8 413; C3's Cornell kernel does not take it)
+  // box_first/64 of the live lanes are at BVH nodes (4-wide nodes count; measured on C4 at 100 spp, round
+  // 2: 64 (never) 430 ms, 48 416, 32 406, 16 398, 8 413; round 5, hoisted media and one 4-wide tree, with
+  // trav_stop 8: 0 189.6, 2 178.6, 4 174.6, 8 176.3, 16 182.3, 32 185.3; C3's Cornell kernel does not
+  // take it)
   const char* box_env = std::getenv("RTAMD_BOX_FIRST");
-  A.box_first = box_env ? std::max(0, std::min(64, std::atoi(box_env))) : 16;
+  A.box_first = box_env ? std::max(0, std::min(64, std::atoi(box_env))) : 4;
   const char* med_env = std::getenv("RTAMD_MED_BATCH");
-  // lanes at a medium wait for 4 of them (C4 at 100 spp, same box: 0 249.0 ms, 4 245.3, 8 245.9, 16 295 at
-  // the time's 10-wave occupancy)
-  A.med_batch = med_env ? std::max(0, std::min(64, std::atoi(med_env))) : 4;
+  // lanes at a medium wait for med_batch of them (round 4, C4 at 100 spp: 0 249.0 ms, 4 245.3, 8 245.9,
+  // 16 295). Since round 5 a world's own media are hoisted (RT_BVH_MEDIA_FIRST, taken where walks start):
+  // only media inside instance frames still wait here, none in C4 (0 174.6 ms vs 4 176.3): off by default
+  A.med_batch = med_env ? std::max(0, std::min(64, std::atoi(med_env))) : 0;
   // work order only (the chunk sums do not depend on it): the slab's tiles last to first
   A.rev_tiles = env_off("RTAMD_TILE_REV") || !std::getenv("RTAMD_TILE_REV") ? 0u : (uint32_t)per_shard;
   const unsigned var = variant_for(c->features);
