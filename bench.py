@@ -366,6 +366,7 @@ def main():
 
     # device-measured work of this exact launch (counting build, outside the timed region)
     work = ctx.render_work(cam, p) if not args.no_work else None
+    work_loop = ctx.last_launch()["loop"] if work else None  # (the counting build's walk: 2 = 4-wide, 1 = binary / mixed)
 
     for i in range(args.warmup):
         frame.step()
@@ -451,12 +452,12 @@ def main():
             leaf_hits, tie_redos = work.pop("leaf_hits"), work.pop("tie_redos")
             if slots["outer_iterations"]:  # lane utilisation of the replacement loop's phases
                 out["lane_utilisation"] = {"shade": round(work["segments"] / slots["outer_iterations"], 4)}
-                if work["wide_nodes"] and slots["wide_steps"] and slots["leaf_steps"]:  # (4-wide: two kinds of step)
+                if work_loop == 2 and slots["wide_steps"] and slots["leaf_steps"]:  # (4-wide: two kinds of step)
                     out["lane_utilisation"]["wide_steps"] = round(work["wide_nodes"] / slots["wide_steps"], 4)
                     out["lane_utilisation"]["leaf_steps"] = round(work["prim_tests"] / slots["leaf_steps"], 4)
-                elif slots["wide_steps"]:  # binary walk: node visits per lane slot of its steps, and how many
-                    # node kinds (BVH box, leaf primitive, instance, medium) one step runs on average
-                    visits = work["box_tests"] + work["prim_tests"] + work["other_tests"]
+                elif slots["wide_steps"]:  # binary / mixed walk: node visits per lane slot of its steps, and how
+                    # many node kinds (BVH box or 4-wide node, leaf primitive, instance, medium) one step runs
+                    visits = work["box_tests"] + work["wide_nodes"] + work["prim_tests"] + work["other_tests"]
                     out["lane_utilisation"]["walk_steps"] = round(visits / slots["wide_steps"], 4)
                     out["walk_step_kinds"] = round(slots["leaf_steps"] / slots["wide_steps"], 4)
             per = {k: work[k] / n for k in work}

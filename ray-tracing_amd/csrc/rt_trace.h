@@ -683,18 +683,25 @@ __device__ __forceinline__ void set_ray32(Trav& t, double t_min) {
                    (isinf(t.i32z) & (t.ray.d.z != 0.0)) | isnan(t.i32x) | isnan(t.i32y) | isnan(t.i32z) |
                    !isfinite(t.o32x) | !isfinite(t.o32y) | !isfinite(t.o32z) | isnan(t.slack) |
                    !(t.tmin32 > 0.0f);
+  // A ray with a NaN in its origin or direction (the next segment after a rect hit at t = NaN:
+  // trav_take) hits nothing in the reference — its root box test fails (a NaN slab quotient) — and
+  // here no child is entered (slack -inf): accepting every child instead walked the whole tree for
+  // each such segment (a 400-box field alone: 745 4-wide nodes and 2200 leaf tests per sample), and a
+  // rect leaf would have taken its t = NaN.
+  const bool dead = (t.ray.o.x != t.ray.o.x) | (t.ray.o.y != t.ray.o.y) | (t.ray.o.z != t.ray.o.z) |
+                    (t.ray.d.x != t.ray.d.x) | (t.ray.d.y != t.ray.d.y) | (t.ray.d.z != t.ray.d.z);
   t.o32x = bad ? 0.0f : t.o32x;
   t.o32y = bad ? 0.0f : t.o32y;
   t.o32z = bad ? 0.0f : t.o32z;
   t.i32x = bad ? 0.0f : t.i32x;
   t.i32y = bad ? 0.0f : t.i32y;
   t.i32z = bad ? 0.0f : t.i32z;
-  t.slack = bad ? INFINITY : t.slack;
+  t.slack = dead ? -INFINITY : (bad ? INFINITY : t.slack);
 }
 
 // The mixed walk refreshes the fp32 origin and reciprocals from the fp64 ray at each wide step instead
 // of carrying them across the walk (six registers fewer in the full variant: 240 -> 192 B/lane of
-// scratch); `slack` (carried) is +inf exactly for the rays set_ray32 zeroes.
+// scratch); `slack` (carried) is +-inf exactly for the rays set_ray32 zeroes.
 __device__ __forceinline__ void refresh_ray32(Trav& t) {
   const bool bad = isinf(t.slack);
   t.o32x = bad ? 0.0f : (float)t.ray.o.x;

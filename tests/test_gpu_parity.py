@@ -488,3 +488,37 @@ def test_exact_trace_matches_oracle(gpu_ctx):
         assert len(a) == len(b) > 48 * 4
         assert np.array_equal(a, b, equal_nan=True), f"column {col}: first difference at record " \
             f"{int(np.argmax(~np.all((a == b) | (np.isnan(a) & np.isnan(b)), axis=1)))}"
+
+
+@pytest.mark.parametrize("walk", [rtamd.RT_DEBUG_RESUMABLE, rtamd.RT_DEBUG_WIDE])
+def test_nan_rays_hit_nothing(gpu_ctx, walk):
+    """Rays with a NaN in the origin or direction (the segment after a rect hit at t = NaN, from the
+    Lambertian quirk's +x ray along a box top) hit nothing, as in the reference, whose root box test fails
+    for them: the 4-wide walk's fp32 test rejects every child (set_ray32) instead of accepting them all,
+    which walked the whole tree per segment and let rect leaves take t = NaN. Checked against the oracle
+    with ordinary rays mixed in, and on a tier-B render of the box field: per-sample work stays that of a
+    culling walk (it was 745 4-wide nodes and 2200 leaf tests per sample)."""
+    import nwf_parts
+    sc, _ = nwf_parts.scene(["boxes"])
+    gpu_ctx.upload(sc)
+    rng = np.random.default_rng(5)
+    n = 4096
+    o = rng.uniform(-1000, 1000, (n, 3))
+    o[:, 1] = rng.uniform(0, 300, n)
+    d = rng.normal(0, 1, (n, 3))
+    k = rng.integers(0, 6, n // 2)
+    o[np.arange(n // 2)[k < 3], k[k < 3]] = np.nan
+    d[np.arange(n // 2)[k >= 3], k[k >= 3] - 3] = np.nan
+    rays = np.concatenate([o, d, rng.uniform(0, 1, (n, 1))], axis=1)
+    got = gpu_ctx.closest_hits(rays, 1e-3, np.inf, seed=3, flags=walk)
+    ref = pyoracle.closest_hits(sc, rays, 1e-3, np.inf, seed=3)
+    assert not got[: n // 2, 0].any() and not ref[: n // 2, 0].any()
+    assert got[n // 2:, 0].sum() > n // 8
+    assert np.array_equal(got[:, [0, 1, 2, 3, 4, 5, 6, 7, 10, 11]], ref[:, [0, 1, 2, 3, 4, 5, 6, 7, 10, 11]])
+    if walk == rtamd.RT_DEBUG_WIDE:
+        cam = rtamd.camera("next_week", 96, 96)
+        p = rtamd.make_params(96, 96, 8, 50, rtamd.RT_RNG_PHILOX, seed=1024)
+        w = gpu_ctx.render_work(cam, p)
+        per = {f: w[f] / w["samples"] for f in ("prim_tests", "wide_nodes")}
+        print(f"box field, tier B 96x96x8: {per}")
+        assert per["prim_tests"] < 20 and per["wide_nodes"] < 60
