@@ -34,6 +34,13 @@
 #define RT_SUB 0x20000000   /* node-id tag (walks in the reference's order): inside a re-bounded,
                                media-free subtree (below an RT_BVH_ORDERED node) */
 #define RT_CHAIN_PRIM 0x100 /* device node type flag: Translate/Rotate chain ending in a primitive */
+/* Leaf-table copies of instance frames (mixed walks): the frame chain opened from this leaf is described by
+   the copy itself, so the walk opens it without loading the chain's records. FUSED: one frame (this node),
+   whose child `a` is not an instance frame opened with it; FUSED2: two frames, this one and its child `a`, a
+   Rotate (sin f[3], cos f[4], axis (type >> RT_FRAME_AX2_SHIFT) & 3), whose child is (int)f[5]. */
+#define RT_FRAME_FUSED 0x200
+#define RT_FRAME_FUSED2 0x400
+#define RT_FRAME_AX2_SHIFT 11
 #define RT_TYPE_MASK 0xff
 
 namespace rtd {

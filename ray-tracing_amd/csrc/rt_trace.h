@@ -1168,15 +1168,32 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
     // with one prep() for the innermost ray (the outer frames' rays are not tested against anything)
     Ray cr = plain(t.ray);
     int cur = leaf_slot ? n->c : id, ct = tf;
-    do {
+    if ((F & F_MIXW) && leaf_slot && (tf & RT_FRAME_FUSED)) {
+      // the chain from the leaf-table copy (rt_prepare.cpp fuse_frame): no record loads
       if constexpr ((F & F_COUNT) != 0) ++cnt.other;
       side.frame(t.level++) = cur;
       stk[(t.sp++) * stride] = RT_FRAME | cur;
-      cr = enter_instance(&S.nodes[cur], cr);
-      cur = S.nodes[cur].a;
-      ct = S.nodes[cur].type;
-    } while (((ct & RT_TYPE_MASK) == RT_NODE_TRANSLATE || (ct & RT_TYPE_MASK) == RT_NODE_ROTATE) &&
-             !(ct & RT_CHAIN_PRIM));
+      cr = enter_instance(n, cr);
+      cur = n->a;
+      if (tf & RT_FRAME_FUSED2) {
+        if constexpr ((F & F_COUNT) != 0) ++cnt.other;
+        side.frame(t.level++) = cur;
+        stk[(t.sp++) * stride] = RT_FRAME | cur;
+        const int ax = (tf >> RT_FRAME_AX2_SHIFT) & 3;
+        cr = Ray{unrotate_point(ax, n->f[3], n->f[4], cr.o), unrotate_point(ax, n->f[3], n->f[4], cr.d), cr.tm};
+        cur = (int)n->f[5];
+      }
+    } else {
+      do {
+        if constexpr ((F & F_COUNT) != 0) ++cnt.other;
+        side.frame(t.level++) = cur;
+        stk[(t.sp++) * stride] = RT_FRAME | cur;
+        cr = enter_instance(&S.nodes[cur], cr);
+        cur = S.nodes[cur].a;
+        ct = S.nodes[cur].type;
+      } while (((ct & RT_TYPE_MASK) == RT_NODE_TRANSLATE || (ct & RT_TYPE_MASK) == RT_NODE_ROTATE) &&
+               !(ct & RT_CHAIN_PRIM));
+    }
     t.ray = prep(cr);
     if constexpr ((F & F_MIXW) != 0) set_ray32(t, t_min);
     t.node = cur | tag;

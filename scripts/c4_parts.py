@@ -18,7 +18,8 @@ ctx = rtamd.Context(0)
 cam = rtamd.camera("next_week", 800, 800)
 p = rtamd.make_params(800, 800, a.spp, 50, rtamd.RT_RNG_PHILOX, seed=1024)
 cases = [("all", ALL)] + [("-" + g, [x for x in ALL if x != g]) for g in ALL] + [
-    ("boxes", ["boxes"]), ("inst", ["inst"]), ("boxes+fog2", ["boxes", "fog2"])]
+    ("boxes", ["boxes"]), ("inst", ["inst"]), ("boxes+fog2", ["boxes", "fog2"]),
+    ("inst_flat", [x for x in ALL if x != "inst"] + ["inst_flat"])]
 for name, parts in cases:
     sc, _ = nwf_parts.scene(parts)
     ctx.upload(sc)

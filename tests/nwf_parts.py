@@ -36,11 +36,18 @@ def scene(parts):
         items.append(b.constantMedium(0.0001, b.constantColor(1, 1, 1), bd))
     if "perlin" in parts:
         items.append(b.sphere((220, 280, 300), 80, b.lambertian(b.makePerlin(0.1))))
-    if "inst" in parts:
+    if "inst" in parts or "inst_flat" in parts:
         white = lam(0.73, 0.73, 0.73)
         rng = np.random.default_rng(1)
-        sp = [b.sphere(tuple(rng.uniform(0, 165, 3)), 10, white) for _ in range(1000)]
-        items.append(b.translate((-100, 270, 395), b.rotate(rtamd.YAxis, 15, b.makeBVH((0.0, 1.0), sp))))
+        cs = rng.uniform(0, 165, (1000, 3))
+        if "inst" in parts:
+            sp = [b.sphere(tuple(c), 10, white) for c in cs]
+            items.append(b.translate((-100, 270, 395), b.rotate(rtamd.YAxis, 15, b.makeBVH((0.0, 1.0), sp))))
+        else:  # (perf experiments only: the same spheres placed in world space, no instance frame)
+            a = np.radians(15.0)
+            w = np.stack([np.cos(a) * cs[:, 0] + np.sin(a) * cs[:, 2], cs[:, 1],
+                          -np.sin(a) * cs[:, 0] + np.cos(a) * cs[:, 2]], axis=1) + np.array([-100, 270, 395])
+            items.append(b.makeBVH((0.0, 1.0), [b.sphere(tuple(c), 10, white) for c in w]))
     world = b.makeBVH((0.0, 1.0), items) if len(items) > 1 else items[0]
     return b.finish(world, -1, (0.0, 0.0, 0.0)), b.gen
 
