@@ -37,7 +37,9 @@
 /* Leaf-table copies of instance frames (mixed walks): the frame chain opened from this leaf is described by
    the copy itself, so the walk opens it without loading the chain's records. FUSED: one frame (this node),
    whose child `a` is not an instance frame opened with it; FUSED2: two frames, this one and its child `a`, a
-   Rotate (sin f[3], cos f[4], axis (type >> RT_FRAME_AX2_SHIFT) & 3), whose child is (int)f[5]. */
+   Rotate (sin f[3], cos f[4], axis (type >> RT_FRAME_AX2_SHIFT) & 3). Either way (int)f[5] is where the walk
+   goes on inside: the innermost child, or RT_WNODE | the 4-wide tree of that child when it has one (its
+   children's fp32 boxes cull what its own exact box test would). */
 #define RT_FRAME_FUSED 0x200
 #define RT_FRAME_FUSED2 0x400
 #define RT_FRAME_AX2_SHIFT 11

@@ -174,20 +174,22 @@ unsigned scene_features(const rt_scene_desc* d) {
 // An instance frame's leaf-table copy describes the frames it opens (RT_FRAME_FUSED, rt_layout.h): the
 // mixed walk then opens them from the copy it has loaded already instead of loading each record of the
 // chain in turn (C4: translate (rotate (1000 spheres))).
-void fuse_frame(const std::vector<rt_node>& flat, rt_node& leaf) {
+void fuse_frame(const std::vector<rt_node>& flat, const std::vector<int>& wroot, rt_node& leaf) {
   auto is_frame = [&](const rt_node& x) {
     const int ty = x.type & RT_TYPE_MASK;
     return (ty == RT_NODE_TRANSLATE || ty == RT_NODE_ROTATE) && !(x.type & RT_CHAIN_PRIM);
   };
   if (!is_frame(leaf)) return;
+  auto target = [&](int id) { return (double)(wroot[id] >= 0 ? (RT_WNODE | wroot[id]) : id); };
   const rt_node& c1 = flat[leaf.a];
   if (!is_frame(c1)) {
     leaf.type |= RT_FRAME_FUSED;
+    leaf.f[5] = target(leaf.a);
   } else if ((c1.type & RT_TYPE_MASK) == RT_NODE_ROTATE && !is_frame(flat[c1.a]) && c1.b >= 0 && c1.b <= 2) {
     leaf.type |= RT_FRAME_FUSED | RT_FRAME_FUSED2 | (c1.b << RT_FRAME_AX2_SHIFT);
     leaf.f[3] = c1.f[0];
     leaf.f[4] = c1.f[1];
-    leaf.f[5] = (double)c1.a;
+    leaf.f[5] = target(c1.a);
   }
 }
 
@@ -261,7 +263,7 @@ void mixed_wide_trees(PreparedScene& P, const std::vector<rt_node>& host, const 
         leaves.push_back(flat[id]);
         leaves.back().c = id;
         if ((flat[id].type & RT_TYPE_MASK) == RT_NODE_MOVING_SPHERE) leaves.push_back(flat[id + 1]);
-        fuse_frame(flat, leaves.back());
+        fuse_frame(flat, wroot, leaves.back());
       }
       w.child[k] = ~slot[id];
 #if RT_FRAME_BATCH

@@ -1174,15 +1174,18 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
       side.frame(t.level++) = cur;
       stk[(t.sp++) * stride] = RT_FRAME | cur;
       cr = enter_instance(n, cr);
-      cur = n->a;
       if (tf & RT_FRAME_FUSED2) {
         if constexpr ((F & F_COUNT) != 0) ++cnt.other;
-        side.frame(t.level++) = cur;
-        stk[(t.sp++) * stride] = RT_FRAME | cur;
+        side.frame(t.level++) = n->a;
+        stk[(t.sp++) * stride] = RT_FRAME | n->a;
         const int ax = (tf >> RT_FRAME_AX2_SHIFT) & 3;
         cr = Ray{unrotate_point(ax, n->f[3], n->f[4], cr.o), unrotate_point(ax, n->f[3], n->f[4], cr.d), cr.tm};
-        cur = (int)n->f[5];
       }
+      const int inner = (int)n->f[5];
+      t.ray = prep(cr);
+      set_ray32(t, t_min);
+      t.node = (inner & RT_WNODE) ? inner : (inner | tag);  // (a 4-wide root carries no tag)
+      return true;
     } else {
       do {
         if constexpr ((F & F_COUNT) != 0) ++cnt.other;
