@@ -222,6 +222,33 @@ __device__ __forceinline__ bool sphere_t(V3 sc, double sr, const RayX& r, double
   else return false;
   return true;
 }
+// A ConstantMedium's two boundary queries (Lib.hs:1062-1065) on a sphere boundary in one go: t1 = the
+// sphere's t over (-inf, inf), t2 = its t over (t1 + eps, inf). Both queries compute the same quotients;
+// this evaluates them once and applies the two range tests of sphere_t.
+__device__ __forceinline__ bool sphere_t12(V3 sc, double sr, const RayX& r, double& t1, double& t2) {
+  const V3 oc = r.o - sc;
+  const double a = r.d.x * r.d.x + r.d.y * r.d.y + r.d.z * r.d.z;
+  const double inva = 1.0 / a;
+  const double b = dot(oc, r.d);
+  const double c = dot(oc, oc) - (sr * sr);
+  const double disc = b * b - a * c;
+  if (!(disc > 0)) return false;
+  const double sd = sqrt(disc);
+  const double n1 = (-b) - sd, n2 = (-b) + sd;
+  double temp1 = div_mk(n1, a, inva), temp2 = div_mk(n2, a, inva);
+  if (!(in_range(a) & q_ok(n1, temp1) & q_ok(n2, temp2))) {
+    temp1 = n1 / a;
+    temp2 = n2 / a;
+  }
+  if (-INFINITY < temp1 && temp1 < INFINITY) t1 = temp1;
+  else if (-INFINITY < temp2 && temp2 < INFINITY) t1 = temp2;
+  else return false;
+  const double lo = t1 + kEps;
+  if (lo < temp1 && temp1 < INFINITY) t2 = temp1;
+  else if (lo < temp2 && temp2 < INFINITY) t2 = temp2;
+  else return false;
+  return true;
+}
 // log for hit ConstantMedium's distance draw (Lib.hs:1074). Not inlined, like sphere_uv: the draw happens
 // inside the walk, and OCML's fp64 log coefficients held across the render loop cost the full variant
 // 304 -> 240 B/lane of scratch (C4 at 100 spp 323.5 -> 306.6 ms: the spill footprint is what
@@ -870,8 +897,13 @@ __device__ __forceinline__ double hoisted_medium_t(const rt_node* nodes, int id,
   S.nodes = nodes;
   const rt_node* n = &nodes[id];
   double t1, t2;
-  if (!chain_tx<F>(S, n->a, rx, -INFINITY, INFINITY, t1)) return -1.0;
-  if (!chain_tx<F>(S, n->a, rx, t1 + kEps, INFINITY, t2)) return -1.0;
+  const rt_node* bd = &nodes[n->a];
+  if (bd->type == RT_NODE_SPHERE) {  // (one quadratic for both boundary queries)
+    if (!sphere_t12(vload(bd->f), bd->f[3], rx, t1, t2)) return -1.0;
+  } else {
+    if (!chain_tx<F>(S, n->a, rx, -INFINITY, INFINITY, t1)) return -1.0;
+    if (!chain_tx<F>(S, n->a, rx, t1 + kEps, INFINITY, t2)) return -1.0;
+  }
   const double rec1tp = gmax(t_min, t1);
   if (rec1tp >= t2) return -1.0;
   const double rec1t = rec1tp < 0 ? 0 : rec1tp;
