@@ -392,6 +392,10 @@ int rt_rebuild_bvh(const rt_scene_desc* desc, rt_node* out_nodes, int capacity, 
  * = the walk's stack bound (entries). RT_E_UNSUPPORTED when the root is not a BVH node. */
 int rt_wide_bvh(const rt_node* nodes, int n_nodes, int root, void* out, int capacity, int* out_n,
                 int* out_stack_need);
+/* The 64-byte quantised form (rt_qnode, rt_wide.h) of n 4-wide records (rt_wide_bvh output) that the
+ * kernels reading the tree from global memory walk: out holds n records. RT_E_UNSUPPORTED when a node's
+ * boxes cannot be put on an fp32 grid (planes beyond fp32 range). */
+int rt_quantize_wide(const void* wnodes, int n, void* out);
 /* The host half of rt_upload_scene, with no device: validates `desc` exactly as the upload does
  * (same error codes and rt_last_error text; RT_UPLOAD_REFERENCE_BVH as for the upload) and describes
  * the device copy it would upload. Malformed descriptors can be checked on a machine without a GPU. */
@@ -503,6 +507,8 @@ int rt_last_launch(rt_ctx* ctx, rt_launch_info* out);
  */
 #define RT_DEBUG_RESUMABLE 4u
 #define RT_DEBUG_WIDE 8u
+#define RT_DEBUG_QNODE 16u /* the 4-wide walk over the quantised tree (rt_qnode) and sphere quadruples that the
+                              global-memory kernels of spheres-only worlds take */
 int rt_debug_closest_hits(rt_ctx* ctx, const double* rays, int n, double tmin, double tmax,
                           uint64_t seed, uint32_t flags, double* out);
 

@@ -20,6 +20,23 @@ typedef struct rt_wnode {
   int32_t pad[RT_WIDE];
 } rt_wnode;
 
+// The same node with its child boxes quantised to 8 bits per plane against a per-node grid (64 bytes:
+// half an L2 line; the kernels that read the tree from global memory, where the 100k-sphere world's
+// nodes and leaves do not fit an XCD's L2). Per axis a, plane q of child k is origin[a] + q * scale[a]
+// exactly in fp32: scale is a power of two and origin an integer multiple of it below 2^23 * scale, so
+// the decoded boxes are fp32 planes containing the node's fp32 boxes (lo rounded down, hi up to the grid)
+// and the fp32 test over them culls conservatively, as over rt_wnode's. qlo[a] / qhi[a] hold child k's
+// lower / upper plane in byte k. An unused slot has qlo 255 and qhi 0 on every axis (an empty box) and
+// refers to a leaf of this node, as in rt_wnode.
+typedef struct rt_qnode {
+  float origin[3];
+  float scale[3];
+  uint32_t qlo[3];
+  uint32_t qhi[3];
+  int32_t child[RT_WIDE];
+} rt_qnode;
+
 #ifdef __cplusplus
 static_assert(sizeof(rt_wnode) == 128, "rt_wnode is 128 bytes");
+static_assert(sizeof(rt_qnode) == 64, "rt_qnode is 64 bytes");
 #endif

@@ -729,7 +729,97 @@ int rebuild_for_device(std::vector<rt_node>& nodes, int root) {
   return rebuild_media_skeleton(nodes, root);
 }
 
+// rt_qnode (rt_wide.h) from rt_wnode: per node and axis a power-of-two grid step s and an origin on the
+// grid (k s, |k| < 2^23) below every child's lower plane, with the node's planes within 255 steps; each
+// child's fp32 box is rounded outward to the grid. False when a node's planes do not fit an fp32 grid.
+bool quantize_wide(const std::vector<rt_wnode>& in, std::vector<rt_qnode>& out) {
+  out.assign(in.size(), rt_qnode{});
+  for (size_t i = 0; i < in.size(); ++i) {
+    const rt_wnode& w = in[i];
+    rt_qnode& q = out[i];
+    for (int k = 0; k < RT_WIDE; ++k) q.child[k] = w.child[k];
+    for (int a = 0; a < 3; ++a) {
+      double L = INFINITY, H = -INFINITY;
+      for (int k = 0; k < RT_WIDE; ++k)
+        if (w.lo[a][k] <= w.hi[a][k]) {  // (an unused slot has lo = +inf, hi = -inf)
+          L = std::min(L, (double)w.lo[a][k]);
+          H = std::max(H, (double)w.hi[a][k]);
+        }
+      uint32_t qlo = 0, qhi = 0;
+      if (!(L <= H)) {  // no child box on this axis (every slot unused)
+        q.origin[a] = 0.0f;
+        q.scale[a] = 1.0f;
+        for (int k = 0; k < RT_WIDE; ++k) qlo |= 255u << (8 * k);
+        q.qlo[a] = qlo;
+        q.qhi[a] = 0;
+        continue;
+      }
+      if (!std::isfinite(L) || !std::isfinite(H)) return false;
+      int e = -126;
+      {
+        const double span = (H - L) / 254.0, mag = std::max(std::fabs(L), std::fabs(H)) / 8388352.0;
+        const double need = std::max(span, mag);
+        if (need > 0) e = std::max(e, (int)std::ceil(std::log2(need)));
+      }
+      double s = 0, org = 0;
+      for (;; ++e) {
+        if (e > 127) return false;
+        s = std::ldexp(1.0, e);
+        const double kk = std::floor(L / s);
+        org = kk * s;
+        // (every plane the node can decode, org + q s for q <= 255, stays a finite fp32 value)
+        if (std::fabs(kk) + 256.0 < 8388608.0 && std::ceil((H - org) / s) <= 255.0 &&
+            org + 255.0 * s <= 3.4028234663852886e38)
+          break;
+      }
+      q.origin[a] = (float)org;  // (exact: |kk| < 2^23, s a normal power of two)
+      q.scale[a] = (float)s;
+      for (int k = 0; k < RT_WIDE; ++k) {
+        uint32_t lo = 255, hi = 0;
+        if (w.lo[a][k] <= w.hi[a][k]) {
+          lo = (uint32_t)std::floor(((double)w.lo[a][k] - org) / s);
+          hi = (uint32_t)std::ceil(((double)w.hi[a][k] - org) / s);
+        } else {
+          // an unused slot: empty on every axis
+          lo = 255;
+          hi = 0;
+        }
+        qlo |= lo << (8 * k);
+        qhi |= hi << (8 * k);
+      }
+      q.qlo[a] = qlo;
+      q.qhi[a] = qhi;
+    }
+    // an unused slot stays empty on every axis even where this axis saw no box at all
+    for (int k = 0; k < RT_WIDE; ++k) {
+      bool used = true;
+      for (int a = 0; a < 3; ++a) used &= w.lo[a][k] <= w.hi[a][k];
+      if (!used)
+        for (int a = 0; a < 3; ++a) {
+          q.qlo[a] = (q.qlo[a] & ~(255u << (8 * k))) | (255u << (8 * k));
+          q.qhi[a] &= ~(255u << (8 * k));
+        }
+    }
+  }
+  return true;
+}
+
 }  // namespace rt
+
+extern "C" int rt_quantize_wide(const void* wnodes, int n, void* out) {
+  if (!wnodes || !out || n < 0) {
+    rt::set_error("rt_quantize_wide: bad argument");
+    return RT_E_INVALID;
+  }
+  const rt_wnode* w = static_cast<const rt_wnode*>(wnodes);
+  std::vector<rt_qnode> q;
+  if (!rt::quantize_wide(std::vector<rt_wnode>(w, w + n), q)) {
+    rt::set_error("rt_quantize_wide: a node's boxes do not fit an fp32 grid");
+    return RT_E_UNSUPPORTED;
+  }
+  std::copy(q.begin(), q.end(), static_cast<rt_qnode*>(out));
+  return RT_OK;
+}
 
 extern "C" int rt_rebuild_bvh(const rt_scene_desc* in, rt_node* out_nodes, int capacity, int* out_n, int* out_root) {
   if (!in || !out_n || !out_root || !in->nodes || in->n_nodes <= 0 || in->world_root < 0 ||

@@ -148,6 +148,8 @@ struct Scene {
   const rt_node* nodes;
   const rt_wnode* wnodes;  // 4-wide world tree (F_WIDE kernels); null when not built
   const rt_node* leaves;   // its leaf table: referenced leaves (c = flat node id), LDS or global
+  const rt_qnode* qnodes;  // spheres-only worlds: the 4-wide tree quantised (F_QNODE kernels), or null
+  const double* sleaves;   // and its leaf table's spheres: center xyz, radius per slot
   const DMat* mats;
   const rt_texture* texs;
   const rt_perlin* perlins;

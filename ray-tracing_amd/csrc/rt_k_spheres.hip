@@ -3,7 +3,7 @@
 #include "rt_kernels.h"
 
 namespace rt {
-const void* philox_kernel_spheres(int loop, bool lds, int w, bool count, bool leaf_lds) {
-  return pick<kVarSpheres>(loop, lds, w, count, leaf_lds);
+const void* philox_kernel_spheres(int loop, bool lds, int w, bool count, bool leaf_lds, bool q) {
+  return pick<kVarSpheres>(loop, lds, w, count, leaf_lds, q);
 }
 }  // namespace rt

@@ -845,7 +845,15 @@ __global__ void math_probe(int op, const double* x, const double* y, int n, doub
 // sample per lane walk, 1 = ray replacement over the binary tree, 2 = replacement over the
 // 4-wide tree.
 template <unsigned V>
-const void* pick_w(bool lds, int w, bool leaf_lds = false) {
+const void* pick_w(bool lds, int w, bool leaf_lds = false, bool q = false) {
+  if constexpr (V == (kVarSpheres | F_WIDE)) {
+    if (!lds && q) {  // (the quantised tree and sphere quadruples from global memory)
+      if (w == 2) return (const void*)render_philox2<V | F_QNODE, 2>;
+      if (w == 3) return (const void*)render_philox2<V | F_QNODE, 3>;
+      if (w == 4) return (const void*)render_philox2<V | F_QNODE, 4>;
+      return (const void*)render_philox2<V | F_QNODE, 1>;
+    }
+  }
   if constexpr ((V & F_WIDE) != 0) {
     if (lds && leaf_lds) {
       if (w == 4) return (const void*)render_philox2_lds<V, 4, true>;
@@ -865,12 +873,15 @@ const void* pick_w(bool lds, int w, bool leaf_lds = false) {
   return (const void*)render_philox2<V, 1>;
 }
 template <unsigned V>
-const void* pick(int loop, bool lds, int w, bool count, bool leaf_lds) {
+const void* pick(int loop, bool lds, int w, bool count, bool leaf_lds, bool q = false) {
   if (count) {
+    if constexpr (V == kVarSpheres) {
+      if (loop == 2 && q) return (const void*)render_philox2<V | F_WIDE | F_COUNT | F_QNODE, 1>;
+    }
     if (loop == 2) return (const void*)render_philox2<V | F_WIDE | F_COUNT, 1>;
     return loop ? (const void*)render_philox2<V | F_COUNT, 1> : (const void*)render_philox<V | F_COUNT, 1>;
   }
-  if (loop == 2) return pick_w<V | F_WIDE>(lds, w, leaf_lds);
+  if (loop == 2) return pick_w<V | F_WIDE>(lds, w, leaf_lds, q);
   if (loop == 1) return pick_w<V>(lds, w);
   if (lds) {
     if (w == 2) return (const void*)render_philox_lds<V, 2>;
@@ -901,7 +912,7 @@ const void* pick_full(int loop, bool lds, int w, bool count) {
 // Render-kernel tables, one per kernel translation unit: the kernel for (loop, LDS-staged?, waves per
 // SIMD, counting build?, leaf table in LDS?) of that unit's variant(s).
 namespace rt {
-const void* philox_kernel_spheres(int loop, bool lds, int w, bool count, bool leaf_lds);
+const void* philox_kernel_spheres(int loop, bool lds, int w, bool count, bool leaf_lds, bool q);
 const void* philox_kernel_cornell(int loop, bool lds, int w, bool count, bool leaf_lds);
 const void* philox_kernel_full(int loop, bool lds, int w, bool count);
 const void* philox_kernel_full_dark(int loop, bool lds, int w, bool count);

@@ -62,8 +62,10 @@ enum : unsigned {
   F_WIDE = 256u,  // resumable walk over the 4-wide fp32-box tree (rt_wide.h) instead of the binary one
   F_MIXW = 1024u, // the mixed walk (media / frame worlds) enters 4-wide fp32-box trees built over the
                   // re-bounded subtrees (RT_WROOT nodes) instead of walking them node by node
-  F_SLIBM = 2048u // tier A with RT_FLAG_SHARED_LIBM: sin / cos / log / atan / asin from include/rt_libm.h
-                  // (the oracle's too) instead of OCML
+  F_SLIBM = 2048u, // tier A with RT_FLAG_SHARED_LIBM: sin / cos / log / atan / asin from include/rt_libm.h
+                   // (the oracle's too) instead of OCML
+  F_QNODE = 4096u  // (spheres-only F_WIDE kernels reading the tree from global memory) the quantised 4-wide
+                   // nodes (rt_qnode) and the leaves' sphere quadruples instead of the 128 / 64-byte records
 };
 
 // Kernel variants: spheres-only (configs 1, 2, 5), Cornell-like (rects, instances, lights), full.

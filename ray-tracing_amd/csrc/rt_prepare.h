@@ -16,6 +16,10 @@ struct PreparedScene {
   std::vector<rtd::DMat> mats;    // device materials
   std::vector<rt_wnode> wnodes;   // 4-wide trees: the world's (media-free worlds) or the re-bounded subtrees'
   std::vector<rt_node> leaves;    // their leaf table (c = flat node id)
+  // spheres-only worlds with a 4-wide world tree: the same tree quantised (rt_qnode, 64 B) and the leaf
+  // table's spheres as (center, radius) quadruples, for the kernels that read them from global memory
+  std::vector<rt_qnode> qnodes;
+  std::vector<double> sleaves;
   int world = 0, world_ref = 0;   // walk roots (with RT_ISBOX): the device tree's and the caller's
   int world_root = 0;             // the device tree's root id (untagged)
   int lights = -1;

@@ -54,6 +54,8 @@ struct rt_ctx {
   int stack_need = 0;  // deepest traversal stack the world tree needs (entries)
   rt_wnode* d_wnodes = nullptr;  // 4-wide world tree (replace_ok worlds with a BVH root)
   rt_node* d_leaves = nullptr;   // its leaf table (Scene::leaves)
+  rt_qnode* d_qnodes = nullptr;  // spheres-only worlds: the 4-wide tree quantised (Scene::qnodes)
+  double* d_sleaves = nullptr;   // and the leaf table's spheres (Scene::sleaves)
   int n_leaves = 0;
   int n_wnodes = 0;
   int wide_stack_need = 0;
@@ -148,8 +150,12 @@ void free_scene(rt_ctx* c) {
   (void)hipFree(c->d_pool);
   (void)hipFree(c->d_wnodes);
   (void)hipFree(c->d_leaves);
+  (void)hipFree(c->d_qnodes);
+  (void)hipFree(c->d_sleaves);
   c->d_wnodes = nullptr;
   c->d_leaves = nullptr;
+  c->d_qnodes = nullptr;
+  c->d_sleaves = nullptr;
   c->mixed_wide = false;
   c->n_leaves = 0;
   c->n_wnodes = 0;
@@ -212,8 +218,8 @@ int waves_target(int dflt) {
   return (w >= 1 && w <= 4) ? w : dflt;
 }
 // (the render kernels live in one translation unit per variant: rt_k_*.hip)
-const void* philox_kernel(unsigned var, int loop, bool lds, int w, bool count, bool leaf_lds = false) {
-  if (var == kVarSpheres) return rt::philox_kernel_spheres(loop, lds, w, count, leaf_lds);
+const void* philox_kernel(unsigned var, int loop, bool lds, int w, bool count, bool leaf_lds = false, bool q = false) {
+  if (var == kVarSpheres) return rt::philox_kernel_spheres(loop, lds, w, count, leaf_lds, q);
   if (var == kVarCornell) return rt::philox_kernel_cornell(loop, lds, w, count, leaf_lds);
   if (var == kVarFullDark) return rt::philox_kernel_full_dark(loop, lds, w, count);
   return rt::philox_kernel_full(loop, lds, w, count);
@@ -431,7 +437,9 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
       return run(fn, dim3(c->cu_count), dim3(block), bytes, args);
     }
   }
-  const void* fn = philox_kernel(var, loop, false, count ? 1 : waves, count);
+  // (spheres-only worlds uploaded with RTAMD_QNODE=1 read the 4-wide tree from global memory in its
+  // 64-byte quantised form: A/B only, measured slower)
+  const void* fn = philox_kernel(var, loop, false, count ? 1 : waves, count, false, loop == 2 && c->d_qnodes);
   // replacement loops: lane stacks (+ Side slots) in dynamic LDS, sized for this world's stack bound
   int entries = wide ? c->wide_stack_need + 3 : c->stack_need + 2;  // (wide_node writes 3 slots)
   const size_t dyn = loop ? (size_t)(entries + side_ints) * RT_BLOCK * sizeof(int) : 0;
@@ -699,7 +707,9 @@ int upload_prepared(rt_ctx* c, const rt::PreparedScene& P, const rt_scene_desc* 
       (rc = upload(&c->d_images, din->images, (size_t)din->n_images)) ||
       (rc = upload(&c->d_pool, din->image_pool, (size_t)din->image_pool_bytes)) ||
       (rc = upload(&c->d_wnodes, P.wnodes.data(), P.wnodes.size())) ||
-      (rc = upload(&c->d_leaves, P.leaves.data(), P.leaves.size()))) {
+      (rc = upload(&c->d_leaves, P.leaves.data(), P.leaves.size())) ||
+      (rc = upload(&c->d_qnodes, P.qnodes.data(), P.qnodes.size())) ||
+      (rc = upload(&c->d_sleaves, P.sleaves.data(), P.qnodes.empty() ? 0 : P.sleaves.size()))) {
     free_scene(c);
     return rc;
   }
@@ -712,6 +722,8 @@ int upload_prepared(rt_ctx* c, const rt::PreparedScene& P, const rt_scene_desc* 
   S.pool = c->d_pool;
   S.wnodes = c->d_wnodes;
   S.leaves = c->d_leaves;
+  S.qnodes = c->d_qnodes;
+  S.sleaves = c->d_sleaves;
   S.world = P.world;
   S.world_ref = P.world_ref;
   S.lights = P.lights;
@@ -965,9 +977,9 @@ int rt_debug_closest_hits(rt_ctx* c, const double* rays, int n, double tmin, dou
     rt::set_error("rt_debug_closest_hits: no scene uploaded");
     return RT_E_STATE;
   }
-  if ((flags & (RT_DEBUG_RESUMABLE | RT_DEBUG_WIDE)) && !c->replace_ok)
+  if ((flags & (RT_DEBUG_RESUMABLE | RT_DEBUG_WIDE | RT_DEBUG_QNODE)) && !c->replace_ok)
     return unsupported("rt_debug_closest_hits: the resumable walks need a world without media and frames");
-  if ((flags & RT_DEBUG_WIDE) && !c->d_wnodes)
+  if ((flags & (RT_DEBUG_WIDE | RT_DEBUG_QNODE)) && !c->d_wnodes)
     return unsupported("rt_debug_closest_hits: no 4-wide tree for this world");
   if (n == 0) return RT_OK;
   DEVICE_SCOPE(c->device);
@@ -979,7 +991,12 @@ int rt_debug_closest_hits(rt_ctx* c, const double* rays, int n, double tmin, dou
   HIPCHK(hipMemcpy(d_rays, rays, sizeof(double) * 7 * (size_t)n, hipMemcpyHostToDevice));
   const int joint = !(flags & RT_FLAG_REFERENCE_CULL);
   const dim3 grid((n + RT_BLOCK - 1) / RT_BLOCK);
-  if (flags & RT_DEBUG_WIDE)
+  if ((flags & RT_DEBUG_QNODE) && !c->d_qnodes)
+    return unsupported("rt_debug_closest_hits: no quantised 4-wide tree for this world (spheres-only worlds)");
+  if (flags & RT_DEBUG_QNODE)
+    hipLaunchKernelGGL(closest_hits<F_UV | F_WIDE | F_QNODE>, grid, dim3(RT_BLOCK), 0, c->stream, c->scene, d_rays, n,
+                       tmin, tmax, seed, joint, 1, d_out);
+  else if (flags & RT_DEBUG_WIDE)
     hipLaunchKernelGGL(closest_hits<F_ALL | F_UV | F_WIDE>, grid, dim3(RT_BLOCK), 0, c->stream, c->scene, d_rays, n,
                        tmin, tmax, seed, joint, 1, d_out);
   else

@@ -944,6 +944,18 @@ __device__ __forceinline__ void trav_media_first(const Scene& S, Trav& t, double
 template <unsigned F, class R>
 __device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, const rt_node* n, int id, double t_min, Cnt& cnt,
                                           R& g, Side& side, bool refsem) {
+  if constexpr ((F & F_QNODE) != 0) {
+    if (id & kSlotTag) {  // a leaf-table slot of a spheres-only world: its (center, radius) quadruple
+      if constexpr ((F & F_COUNT) != 0) ++cnt.prim;
+      const double2* q = reinterpret_cast<const double2*>(S.sleaves + 4 * (size_t)(id & ~kSlotTag));
+      const double2 c01 = q[0], c2r = q[1];
+      double tt;
+      if (!sphere_t(v3(c01.x, c01.y, c2r.x), c2r.y, t.ray, t_min, refsem ? t.closest : closest_up<F>(t), tt)) return;
+      if constexpr ((F & F_COUNT) != 0) ++cnt.phit;
+      trav_take<F>(S, t, tt, id, 0, side, refsem, n, true);
+      return;
+    }
+  }
   const int type = n->type & RT_TYPE_MASK;
   const bool chain = (F & F_INST) && (type == RT_NODE_TRANSLATE || type == RT_NODE_ROTATE);
   const bool medium = (F & F_MEDIA) && type == RT_NODE_CONSTANT_MEDIUM;  // (always on the skeleton: refsem)
@@ -1055,19 +1067,46 @@ __device__ __forceinline__ void cswap(float& ka, int& ca, float& kb, int& cb) {
   ca = c;
 }
 
+// The four planes of one axis of a quantised node (rt_qnode): origin + q * scale, exact in fp32.
+__device__ __forceinline__ float4 qplanes(uint32_t q, float s, float o) {
+  return float4{fmaf((float)(q & 255u), s, o), fmaf((float)((q >> 8) & 255u), s, o),
+                fmaf((float)((q >> 16) & 255u), s, o), fmaf((float)(q >> 24), s, o)};
+}
+
 // One wide node (index `w`): test the four child boxes, enter the nearest accepted child, stack the
-// others (farthest deepest).
+// others (farthest deepest). F_QNODE: the node is read in its quantised form (64 bytes) and its planes
+// decoded; the test over them is the same.
+template <unsigned F = 0>
 __device__ __forceinline__ bool wide_node(const Scene& S, Trav& t, int* stk, int stride, int w) {
-  const float* base = reinterpret_cast<const float*>(&S.wnodes[w]);
-  // (a ray running towards -axis a has the box's hi as its near plane on that axis)
-  const int ox = signbit(t.i32x) ? 12 : 0, oy = signbit(t.i32y) ? 16 : 4, oz = signbit(t.i32z) ? 20 : 8;
-  const float4 nx = *reinterpret_cast<const float4*>(base + ox);
-  const float4 ny = *reinterpret_cast<const float4*>(base + oy);
-  const float4 nz = *reinterpret_cast<const float4*>(base + oz);
-  const float4 fx = *reinterpret_cast<const float4*>(base + (ox ^ 12));
-  const float4 fy = *reinterpret_cast<const float4*>(base + (oy < 12 ? oy + 12 : oy - 12));
-  const float4 fz = *reinterpret_cast<const float4*>(base + (oz < 12 ? oz + 12 : oz - 12));
-  const int4 ch = *reinterpret_cast<const int4*>(base + 24);
+  float4 nx, ny, nz, fx, fy, fz;
+  int4 ch;
+  if constexpr ((F & F_QNODE) != 0) {
+    const uint4* qb = reinterpret_cast<const uint4*>(&S.qnodes[w]);
+    const uint4 a = qb[0], b = qb[1], c = qb[2];
+    const uint4 d = qb[3];
+    ch = int4{(int)d.x, (int)d.y, (int)d.z, (int)d.w};
+    const float ox = __uint_as_float(a.x), oy = __uint_as_float(a.y), oz = __uint_as_float(a.z);
+    const float sx = __uint_as_float(a.w), sy = __uint_as_float(b.x), sz = __uint_as_float(b.y);
+    // (qlo x, y, z = b.z, b.w, c.x; qhi x, y, z = c.y, c.z, c.w; a ray towards -axis: hi is the near plane)
+    const bool mx = signbit(t.i32x), my = signbit(t.i32y), mz = signbit(t.i32z);
+    nx = qplanes(mx ? c.y : b.z, sx, ox);
+    fx = qplanes(mx ? b.z : c.y, sx, ox);
+    ny = qplanes(my ? c.z : b.w, sy, oy);
+    fy = qplanes(my ? b.w : c.z, sy, oy);
+    nz = qplanes(mz ? c.w : c.x, sz, oz);
+    fz = qplanes(mz ? c.x : c.w, sz, oz);
+  } else {
+    const float* base = reinterpret_cast<const float*>(&S.wnodes[w]);
+    // (a ray running towards -axis a has the box's hi as its near plane on that axis)
+    const int ox = signbit(t.i32x) ? 12 : 0, oy = signbit(t.i32y) ? 16 : 4, oz = signbit(t.i32z) ? 20 : 8;
+    nx = *reinterpret_cast<const float4*>(base + ox);
+    ny = *reinterpret_cast<const float4*>(base + oy);
+    nz = *reinterpret_cast<const float4*>(base + oz);
+    fx = *reinterpret_cast<const float4*>(base + (ox ^ 12));
+    fy = *reinterpret_cast<const float4*>(base + (oy < 12 ? oy + 12 : oy - 12));
+    fz = *reinterpret_cast<const float4*>(base + (oz < 12 ? oz + 12 : oz - 12));
+    ch = *reinterpret_cast<const int4*>(base + 24);
+  }
   float k0, k1, k2, k3;
   wide_keys2(t, f32x2{nx.x, nx.y}, f32x2{ny.x, ny.y}, f32x2{nz.x, nz.y}, f32x2{fx.x, fx.y}, f32x2{fy.x, fy.y},
              f32x2{fz.x, fz.y}, k0, k1);
@@ -1133,7 +1172,7 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
   if (wide) {
     if (t.node >= 0) {
       if constexpr ((F & F_COUNT) != 0) ++cnt.wide;
-      if (wide_node(S, t, stk, stride, t.node)) return true;
+      if (wide_node<F>(S, t, stk, stride, t.node)) return true;
     } else {
       const rt_node* n = &S.leaves[~t.node];
       trav_leaf<F>(S, t, n, ~t.node | kSlotTag, t_min, cnt, g, side, false);
@@ -1241,7 +1280,7 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
   if constexpr ((F & F_MIXW) != 0) {  // a 4-wide node (RT_WNODE | index)
     if constexpr ((F & F_COUNT) != 0) ++cnt.wide;
     refresh_ray32(t);
-    if (wide_node(S, t, stk, stride, t.node & ~RT_WNODE)) return true;
+    if (wide_node<F>(S, t, stk, stride, t.node & ~RT_WNODE)) return true;
   }
   return trav_pop_mixed<F>(S, t, stk, stride, side);
 }
@@ -1267,7 +1306,7 @@ __device__ __forceinline__ void trav_postpone(Trav& t, const int* stk, int strid
 template <unsigned F>
 __device__ __forceinline__ void wide_inner(const Scene& S, Trav& t, int* stk, int stride, Cnt& cnt) {
   if constexpr ((F & F_COUNT) != 0) ++cnt.wide;
-  if (!wide_node(S, t, stk, stride, t.node)) t.node = trav_pop(t, stk, stride);
+  if (!wide_node<F>(S, t, stk, stride, t.node)) t.node = trav_pop(t, stk, stride);
   trav_postpone(t, stk, stride);
 }
 template <unsigned F, class R>

@@ -36,6 +36,7 @@ RT_FLAG_SHARED_LIBM = 8  # tier A parity aid: the portable include/rt_libm.h tra
 RT_UPLOAD_REFERENCE_BVH = 1
 RT_DEBUG_RESUMABLE = 4  # rt_debug_closest_hits: the render loop's resumable binary walk
 RT_DEBUG_WIDE = 8       # rt_debug_closest_hits: the resumable walk over the 4-wide fp32-box tree
+RT_DEBUG_QNODE = 16     # ... over its quantised form (rt_qnode) with sphere quadruples (spheres-only worlds)
 RT_BVH_ORDERED = 0x40000000
 RT_BVH_MEDIA_FIRST = 0x10000000
 MATH_OPS = {"div": 0, "div_exact": 1, "sqrt": 2, "sin": 3, "cos": 4, "atan": 5, "asin": 6, "log": 7, "pow": 8,
@@ -138,7 +139,7 @@ EXPORTED = [
     "rt_debug_closest_hits", "rt_debug_math", "rt_render_work", "rt_upload_scene_ex", "rt_rebuild_bvh",
     "rt_wide_bvh", "rt_tree_stack_need", "rt_last_launch", "rt_write_pfm", "rt_debug_probe",
     "rt_prepare_scene", "rt_render_step_profile", "rt_create_multi", "rt_ctx_devices", "rt_last_frame_timing",
-    "rt_debug_exact_trace",
+    "rt_debug_exact_trace", "rt_quantize_wide",
 ]
 
 # include/rt_wide.h: one 4-wide node (128 B)
@@ -216,6 +217,7 @@ def lib() -> C.CDLL:
             "rt_upload_scene_ex": (I, [C.c_void_p, P(rt_scene_desc), C.c_uint32]),
             "rt_rebuild_bvh": (I, [P(rt_scene_desc), P(rt_node), I, P(I), P(I)]),
             "rt_wide_bvh": (I, [P(rt_node), I, I, C.c_void_p, I, P(I), P(I)]),
+            "rt_quantize_wide": (I, [C.c_void_p, I, C.c_void_p]),
             "rt_tree_stack_need": (I, [P(rt_node), I, I, P(I)]),
             "rt_last_launch": (I, [C.c_void_p, P(rt_launch_info)]),
             "rt_write_pfm": (I, [P(D), I, I, I, C.c_char_p, C.c_size_t, P(C.c_size_t)]),
@@ -422,6 +424,19 @@ def wide_bvh(scene: Scene, root: Optional[int] = None) -> Tuple[np.ndarray, int]
     _check(lib().rt_wide_bvh(scene.desc.nodes, scene.desc.n_nodes, r, out.ctypes.data_as(C.c_void_p), n.value,
                              C.byref(n), C.byref(need)), "rt_wide_bvh")
     return out, need.value
+
+
+QNODE_DTYPE = np.dtype([("origin", "<f4", 3), ("scale", "<f4", 3), ("qlo", "<u4", 3), ("qhi", "<u4", 3),
+                        ("child", "<i4", 4)])
+
+
+def quantize_wide(wnodes: np.ndarray) -> np.ndarray:
+    """rt_quantize_wide: the 64-byte quantised form (rt_qnode) of WNODE_DTYPE records."""
+    w = np.ascontiguousarray(wnodes, dtype=WNODE_DTYPE)
+    out = np.zeros(len(w), dtype=QNODE_DTYPE)
+    _check(lib().rt_quantize_wide(w.ctypes.data_as(C.c_void_p), len(w), out.ctypes.data_as(C.c_void_p)),
+           "rt_quantize_wide")
+    return out
 
 
 def tree_stack_need(scene: Scene, root: Optional[int] = None) -> int:

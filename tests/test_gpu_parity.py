@@ -241,12 +241,17 @@ def _special_rays(sc, rng, n):
     return np.concatenate([o, d, rng.uniform(0, 1, (n, 1))], axis=1)
 
 
-@pytest.mark.parametrize("walk", [rtamd.RT_DEBUG_RESUMABLE, rtamd.RT_DEBUG_WIDE])
+@pytest.mark.parametrize("walk", [rtamd.RT_DEBUG_RESUMABLE, rtamd.RT_DEBUG_WIDE, rtamd.RT_DEBUG_QNODE])
 @pytest.mark.parametrize("name", ["random_book_one", "three_spheres", "cornell", "stress_spheres"])
-def test_resumable_walks_closest_hits(gpu_ctx, name, walk):
-    """The render loop's walks (binary resumable; 4-wide with conservative fp32 child boxes) give
-    the oracle's closest hits (the reference's makeBVH tree, fp64 slab tests) on random and
-    adversarial rays: same primitive, t, p, normal bit-identical."""
+def test_resumable_walks_closest_hits(gpu_ctx, name, walk, monkeypatch):
+    """The render loop's walks (binary resumable; 4-wide with conservative fp32 child boxes; the same
+    over the quantised 64-byte nodes and sphere quadruples of spheres-only worlds) give the oracle's
+    closest hits (the reference's makeBVH tree, fp64 slab tests) on random and adversarial rays: same
+    primitive, t, p, normal bit-identical."""
+    if walk == rtamd.RT_DEBUG_QNODE:
+        if name == "cornell":
+            pytest.skip("quantised trees are built for spheres-only worlds")
+        monkeypatch.setenv("RTAMD_QNODE", "1")  # (read at upload)
     sc, _ = _scene(name, param=3000 if name == "stress_spheres" else 0)
     gpu_ctx.upload(sc)
     rng = np.random.default_rng(17)
@@ -522,3 +527,20 @@ def test_nan_rays_hit_nothing(gpu_ctx, walk):
         per = {f: w[f] / w["samples"] for f in ("prim_tests", "wide_nodes")}
         print(f"box field, tier B 96x96x8: {per}")
         assert per["prim_tests"] < 20 and per["wide_nodes"] < 60
+
+
+def test_quantised_tree_renders_the_same_image(gpu_ctx, monkeypatch):
+    """RTAMD_QNODE=1 (A/B: the global-memory spheres kernel over the quantised 64-byte nodes and the
+    32-byte sphere leaves) renders the default build's image, bytes and linear averages."""
+    sc, _ = _scene("stress_spheres", param=3000)
+    cam = rtamd.camera("random_scene", 96, 64)
+    p = rtamd.make_params(96, 64, 4, 50, rtamd.RT_RNG_PHILOX, seed=9)
+    monkeypatch.setenv("RTAMD_LDS", "0")  # (the global-memory kernel in both runs)
+    gpu_ctx.upload(sc)
+    rgb0, lin0, _ = gpu_ctx.render(cam, p, linear=True)
+    monkeypatch.setenv("RTAMD_QNODE", "1")
+    gpu_ctx.upload(sc)
+    rgb1, lin1, _ = gpu_ctx.render(cam, p, linear=True)
+    assert gpu_ctx.last_launch()["loop"] == 2
+    assert np.array_equal(rgb0, rgb1)
+    assert np.array_equal(np.isnan(lin0), np.isnan(lin1)) and np.array_equal(lin0[~np.isnan(lin0)], lin1[~np.isnan(lin1)])
