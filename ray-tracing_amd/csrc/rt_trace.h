@@ -910,7 +910,7 @@ __device__ __forceinline__ double hoisted_medium_t(const rt_node* nodes, int id,
   const double ray_length = vlen(rx.d);
   const double dist_inside = (t2 - rec1t) * ray_length;
   const double rnd = RngPhilox::keyed_at(k0, k1, walk, sample, pid, medium_key(n));
-  const double hit_dist = n->f[0] * log(rnd);
+  const double hit_dist = n->f[0] * log_call(rnd);  // (not inlined: log_call)
   if (hit_dist > dist_inside) return -1.0;
   return rec1t + (hit_dist / ray_length);
 }
