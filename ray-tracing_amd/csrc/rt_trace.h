@@ -1240,19 +1240,28 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
     Ray cr = plain(t.ray);
     int cur = leaf_slot ? n->c : id, ct = tf;
     if ((F & F_MIXW) && leaf_slot && (tf & RT_FRAME_FUSED)) {
-      // the chain from the leaf-table copy (rt_prepare.cpp fuse_frame): no record loads
+      // the chain from the leaf-table copy (rt_prepare.cpp fuse_frame), read whole in one batch of four
+      // 16-byte loads (field by field, the branches on its contents made the loads wait one by one)
+      rt_node rec;
+      {
+        const uint4* q = reinterpret_cast<const uint4*>(n);
+        const uint4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+        uint4* r = reinterpret_cast<uint4*>(&rec);
+        r[0] = q0, r[1] = q1, r[2] = q2, r[3] = q3;
+      }
+      cur = rec.c;
       if constexpr ((F & F_COUNT) != 0) ++cnt.other;
       side.frame(t.level++) = cur;
       stk[(t.sp++) * stride] = RT_FRAME | cur;
-      cr = enter_instance(n, cr);
+      cr = enter_instance(&rec, cr);
       if (tf & RT_FRAME_FUSED2) {
         if constexpr ((F & F_COUNT) != 0) ++cnt.other;
-        side.frame(t.level++) = n->a;
-        stk[(t.sp++) * stride] = RT_FRAME | n->a;
+        side.frame(t.level++) = rec.a;
+        stk[(t.sp++) * stride] = RT_FRAME | rec.a;
         const int ax = (tf >> RT_FRAME_AX2_SHIFT) & 3;
-        cr = Ray{unrotate_point(ax, n->f[3], n->f[4], cr.o), unrotate_point(ax, n->f[3], n->f[4], cr.d), cr.tm};
+        cr = Ray{unrotate_point(ax, rec.f[3], rec.f[4], cr.o), unrotate_point(ax, rec.f[3], rec.f[4], cr.d), cr.tm};
       }
-      const int inner = (int)n->f[5];
+      const int inner = (int)rec.f[5];
       t.ray = prep(cr);
       set_ray32(t, t_min);
       t.node = (inner & RT_WNODE) ? inner : (inner | tag);  // (a 4-wide root carries no tag)
