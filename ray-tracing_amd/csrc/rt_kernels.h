@@ -50,7 +50,8 @@ struct RenderArgs {
   int W, H, spp, max_depth;
   uint32_t flags;
   int tile, tiles_x, tiles_total, shard_rank, shard_count;
-  long long work_total;  // work-items of this shard: slab pixels x sample chunks (< 2^32)
+  long long work_total;  // claimable units of this launch (< 2^32): work-items before tail_start, then one
+                         // unit per sample of each work-item from tail_start on (kTail kernels)
   long long slab;        // slab pixels of this shard
   int chunk, chunks;     // tier B: samples per chunk (rt_sample_chunk) and chunks per pixel in this launch
   int chunk_base;        // the launch's first chunk (a frame may render its chunks in batches)
@@ -78,6 +79,14 @@ struct RenderArgs {
   double* trace;   // tier A, rt_debug_exact_trace: column trace_col's path segments (10 doubles each)
   int* trace_n;
   int trace_col, trace_cap;
+  // (last, so that the fields before keep their kernel-argument offsets in the kernels that do not read
+  // these: moved in the middle, they cost the spheres and Cornell kernels 0.7 %)
+  long long items_total; // work-items of this launch: slab pixels x sample chunks
+  long long tail_start;  // the work-items from here on are dealt one sample per unit (kTail: the frame's
+                         // tail, so that no lane starts a whole chunk of long paths as the GPU runs dry),
+                         // their colours stored in tail_buf and summed in sample order by tail_combine
+  double* tail_buf;      // [unit][3]
+  UDiv div_chunk;        // by chunk
 };
 
 // Slab pixel index -> image pixel (tile-major, 8x8 blocks inside a tile). Slab indices are < 2^32
@@ -114,11 +123,37 @@ __device__ __forceinline__ bool work_item(const RenderArgs& A, uint32_t wi, int&
   slot = (long long)k * A.slab + idx;
   return s0 < s1;
 }
-__device__ __forceinline__ void store_partial(const RenderArgs& A, long long slot, V3 sum) {
-  double* q = A.partial + slot * 3;
+__device__ __forceinline__ void store_partial_at(double* base, long long slot, V3 sum) {
+  double* q = base + slot * 3;
   q[0] = sum.x;
   q[1] = sum.y;
   q[2] = sum.z;
+}
+__device__ __forceinline__ void store_partial(const RenderArgs& A, long long slot, V3 sum) {
+  store_partial_at(A.partial, slot, sum);
+}
+// Sample-granular tails: in the full variants' kernels only (media / frame worlds, C4), whose work-items
+// (8 samples of paths up to 50 segments through fog) are long and uneven — a frame's last claims left
+// C4 a ~19 ms tail per launch. (In the spheres kernel the extra state cost more than its ~2 ms tail:
+// DESIGN.md §3.1.)
+template <unsigned F>
+constexpr bool kTail = (F & F_FRAMES) != 0;
+// A claimable unit: a work-item, or (from tail_start on) one sample of one. A tail unit's slot is
+// kTailSlot + its index (its colour goes to tail_buf); false for pixels outside the image and for units
+// past the work-item's last sample.
+constexpr long long kTailSlot = 1ll << 40;
+__device__ __forceinline__ bool work_unit(const RenderArgs& A, uint32_t wi, int& px, int& row, int& s0, int& s1,
+                                          long long& slot) {
+  if ((long long)wi < A.tail_start) return work_item(A, wi, px, row, s0, s1, slot);
+  const uint32_t u = wi - (uint32_t)A.tail_start;
+  const uint32_t q = udiv(u, A.div_chunk);
+  const uint32_t k = u - q * (uint32_t)A.chunk;
+  if (!work_item(A, (uint32_t)A.tail_start + q, px, row, s0, s1, slot)) return false;
+  s0 += (int)k;
+  if (s0 >= s1) return false;
+  s1 = s0 + 1;
+  slot = kTailSlot + u;
+  return true;
 }
 
 // getRay (Lib.hs:1253-1267): the disk and time draws always happen.
@@ -396,7 +431,9 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     ++s;
     const bool all_nan = (A.flags & RT_FLAG_NAN_CULL) && sum.x != sum.x && sum.y != sum.y && sum.z != sum.z;
     if (s == s_end || all_nan) {
-      store_partial(A, w, sum);
+      // (a tail unit: its one sample's colour, summed in order with its chunk's others by tail_combine)
+      if (kTail<F> && w >= kTailSlot) store_partial_at(A.tail_buf, w - kTailSlot, contrib);
+      else store_partial(A, w, sum);
       w = -1;
     }
   };
@@ -483,7 +520,8 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
           const long long wi = (long long)(rank < avail ? q_next + rank : base2 + (rank - avail));
           if (wi >= A.work_total) {
             done = true;
-          } else if (work_item(A, (uint32_t)wi, px, row, s, s_end, w)) {
+          } else if (kTail<F> ? work_unit(A, (uint32_t)wi, px, row, s, s_end, w)
+                              : work_item(A, (uint32_t)wi, px, row, s, s_end, w)) {
             sum = v3(0, 0, 0);
           } else {
             w = -1;
@@ -615,6 +653,20 @@ __global__ void __launch_bounds__(WAVES * 256, WAVES)
   // launch_philox sizes the dynamic LDS with the same two helpers)
   philox_loop2<F>(A, S, stk, WAVES * 256, stk + stack_entries * WAVES * 256,
                   wave_q[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)]);
+}
+
+// The tail's work-items (work_unit): each chunk's sample colours added in sample order from 0, as the
+// lane that renders a whole chunk adds them (end_sample), into the chunk's slot.
+__global__ void __launch_bounds__(256) tail_combine(RenderArgs A) {
+  const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (j >= A.items_total - A.tail_start) return;
+  int px, row, s0, s1;
+  long long slot;
+  if (!work_item(A, (uint32_t)(A.tail_start + j), px, row, s0, s1, slot)) return;
+  const double* q = A.tail_buf + j * A.chunk * 3;
+  V3 sum = v3(0, 0, 0);
+  for (int k = 0; k < s1 - s0; ++k) sum = sum + v3(q[3 * k], q[3 * k + 1], q[3 * k + 2]);
+  store_partial(A, slot, sum);
 }
 
 // Tier B: a slab pixel's chunk sums added in chunk order, then averaged and stored (rt.h); with chunk

@@ -66,6 +66,8 @@ struct rt_ctx {
   unsigned long long* d_counter = nullptr;
   double* d_partial = nullptr;  // tier-B chunk sums (grown on demand, at most kPartialCap)
   size_t partial_bytes = 0;
+  double* d_tail = nullptr;     // tier-B tail units' sample colours (RenderArgs::tail_buf), grown on demand
+  size_t tail_bytes = 0;
   double* d_acc = nullptr;      // running per-pixel sums of a frame rendered in chunk batches
   size_t acc_bytes = 0;
   double last_ms = 0.0;
@@ -271,6 +273,8 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   if (const char* ce = std::getenv("RTAMD_CHUNK")) A.chunk = std::max(1, std::min(p->spp, std::atoi(ce)));
   A.chunks = (p->spp + A.chunk - 1) / A.chunk;
   A.work_total = slab * A.chunks;  // (the whole frame's; each chunk batch's launch sets its own)
+  A.items_total = A.work_total;
+  A.tail_start = A.work_total;
   A.div_tp = make_udiv((uint32_t)(A.tile * A.tile));
   A.div_tiles_x = make_udiv((uint32_t)A.tiles_x);
   A.div_bpr = make_udiv((uint32_t)(A.tile >> 3));
@@ -317,23 +321,49 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
     A.partial = c->d_partial;
     A.acc = c->d_acc;
   }
-  // (work-item indices are 32-bit on the device, and wave claims may run up to one batch per wave
-  // past the end: keep 2^24 of headroom)
-  if (slab * per_batch >= (1ll << 32) - (1ll << 24))
-    return invalid("image too large: more than 2^32 - 2^24 work-items per shard and launch");
+  // The frame's tail (the full variants' replacement loop, kTail in rt_kernels.h; set below with the
+  // loop): the last `tail_items` work-items of each launch are dealt one sample per unit, their colours
+  // summed in sample order afterwards (tail_combine): the sums rt.h defines, whatever the dealing.
+  // RTAMD_TAIL: tail items per CU (default 768, one per lane of 12 waves; 0: no tail).
+  long long tail_items = 0;
+  A.div_chunk = make_udiv((uint32_t)A.chunk);
+  auto units_of = [&](long long items) { return items + std::min(items, tail_items) * (A.chunk - 1); };
   // one launch per chunk batch (stream-ordered; the events span all of them)
   auto run = [&](const void* fn, dim3 grid, dim3 block, size_t bytes, void** args) -> int {
+    // (work-unit indices are 32-bit on the device, and wave claims may run up to one batch per wave
+    // past the end: keep 2^24 of headroom)
+    if (units_of(slab * per_batch) >= (1ll << 32) - (1ll << 24))
+      return invalid("image too large: more than 2^32 - 2^24 work units per shard and launch");
+    const size_t need_tail = (size_t)std::min(slab * per_batch, tail_items) * (size_t)A.chunk * 3 * sizeof(double);
+    if (need_tail > c->tail_bytes) {
+      HIPCHK(hipEventSynchronize(c->ev_done));
+      (void)hipFree(c->d_tail);
+      c->d_tail = nullptr;
+      c->tail_bytes = 0;
+      HIPCHK(hipMalloc((void**)&c->d_tail, need_tail));
+      c->tail_bytes = need_tail;
+    }
+    A.tail_buf = c->d_tail;
     for (int k0 = 0; k0 < chunks_total; k0 += per_batch) {
       const int nk = std::min(per_batch, chunks_total - k0);
       A.chunk_base = k0;
       A.chunks = nk;
-      A.work_total = slab * nk;
+      A.items_total = slab * nk;
+      A.tail_start = A.items_total - std::min(A.items_total, tail_items);
+      A.work_total = units_of(A.items_total);
       A.div_tile = make_udiv((uint32_t)(A.tile * A.tile * nk));
       A.combine = (k0 > 0 ? 1 : 0) | (k0 + nk == chunks_total ? 2 : 0);
       HIPCHK(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned long long), st));
       if (k0 == 0) HIPCHK(hipEventRecord(c->ev0, st));
       HIPCHK(hipLaunchKernel(fn, grid, block, args, bytes, st));  // (arguments are copied at launch)
       HIPCHK(hipGetLastError());
+      if (A.tail_start < A.items_total) {
+        RenderArgs B = A;
+        void* targs[] = {&B};
+        HIPCHK(hipLaunchKernel((const void*)tail_combine, dim3((unsigned)((A.items_total - A.tail_start + 255) / 256)),
+                               dim3(256), targs, 0, st));
+        HIPCHK(hipGetLastError());
+      }
       if (A.combine & 2) HIPCHK(hipEventRecord(c->ev1, st));
       const int rc = launch_combine(c, A, st);
       if (rc) return rc;
@@ -397,6 +427,10 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   // (the full variant has no 4-wide instantiation: its media-free worlds walk the binary tree)
   const bool wide = replace && c->d_wnodes && !(p->flags & RT_FLAG_REFERENCE_CULL) && want_wide && !is_full(var);
   const int loop = wide ? 2 : (replace ? 1 : 0);
+  if (loop && is_full(var)) {  // (kTail kernels; the per-sample loop claims whole work-items)
+    const char* te = std::getenv("RTAMD_TAIL");
+    tail_items = (long long)c->cu_count * (te ? std::max(0, std::min(1 << 16, std::atoi(te))) : 768);
+  }
   // waves per SIMD (measured): spheres 4 when the LDS-staged kernel fits at 4 (C2 158.4 ms vs
   // 166.6 at 3, 203.2 at 2), else 3 (C5 186.7 ms vs 228.5 at 4, -15 % at 2); Cornell-like on the
   // replacement loop 3 (C3 359.6 ms vs 374.3 at 4, 453.3 at 2), 1 on the per-sample loop; full
@@ -678,6 +712,7 @@ void rt_destroy(rt_ctx* c) {
   free_scene(c);
   (void)hipFree(c->d_counter);
   (void)hipFree(c->d_partial);
+  (void)hipFree(c->d_tail);
   (void)hipFree(c->d_acc);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);

@@ -544,3 +544,35 @@ def test_quantised_tree_renders_the_same_image(gpu_ctx, monkeypatch):
     assert gpu_ctx.last_launch()["loop"] == 2
     assert np.array_equal(rgb0, rgb1)
     assert np.array_equal(np.isnan(lin0), np.isnan(lin1)) and np.array_equal(lin0[~np.isnan(lin0)], lin1[~np.isnan(lin1)])
+
+
+@pytest.mark.parametrize("name,cam", [("next_week_final", "next_week"), ("cornell_smoke", "cornell")])
+def test_tail_units_do_not_change_the_image(gpu_ctx, name, cam, monkeypatch):
+    """The full variants' replacement loop deals the last work-items of a launch one sample per unit
+    (RTAMD_TAIL), their colours summed afterwards in sample order (tail_combine), as the lane that renders
+    a whole chunk sums them: the image and the linear averages are identical with no tail, the default
+    tail, every item in the tail, and every item in the tail with the chunks rendered in batches. At
+    128x96x704 a chunk holds 8 samples (rt_sample_chunk), so tail units are single samples of 8-sample
+    chunks; every sample is rendered once (the counting build's count)."""
+    earth = np.load(_earth_path())["rgb"] if name == "next_week_final" else None
+    sc, _ = _scene(name, earth=earth)
+    c = rtamd.camera(cam, 128, 96)
+    gpu_ctx.upload(sc)
+    p = rtamd.make_params(128, 96, 704, 50, rtamd.RT_RNG_PHILOX, seed=23)
+    slab_chunk = 128 * 96 * 3 * 8
+    out = []
+    for tail, cap in (("0", 0), (None, 0), ("65536", 0), ("65536", 7 * slab_chunk)):
+        if tail is None:
+            monkeypatch.delenv("RTAMD_TAIL", raising=False)
+        else:
+            monkeypatch.setenv("RTAMD_TAIL", tail)
+        if cap:
+            monkeypatch.setenv("RTAMD_PARTIAL_CAP", str(cap))
+        else:
+            monkeypatch.delenv("RTAMD_PARTIAL_CAP", raising=False)
+        out.append(gpu_ctx.render(c, p, linear=True))
+        info = gpu_ctx.last_launch()
+        assert info["loop"] == 1 and info["chunk"] == 8 and info["chunk_batches"] == (13 if cap else 1)
+        assert gpu_ctx.render_work(c, p)["samples"] == 128 * 96 * 704
+    for rgb, lin, _ in out[1:]:
+        assert np.array_equal(rgb, out[0][0]) and np.array_equal(lin, out[0][1], equal_nan=True)
