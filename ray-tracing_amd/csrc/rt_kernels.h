@@ -694,15 +694,37 @@ __global__ void __launch_bounds__(256) combine_chunks(RenderArgs A) {
 // One lane per image column; rows top to bottom; each pixel draws its 2*ns UVs first and uses
 // them in reverse draw order (uniformRandomUVs' foldr, Lib.hs:1358-1371) — the UV pairs are
 // recomputed from the pixel's starting state (SplitMix is seed + k*gamma), no list is stored.
-template <unsigned F>
-__global__ void __launch_bounds__(RT_BLOCK) render_exact(RenderArgs A) {
+// Columns per wave of the tier-A kernel (lanes 0..k-1 of each wave; 64: every lane).
+#ifndef RT_EXACT_COLS_PER_WAVE
+#define RT_EXACT_COLS_PER_WAVE 1
+#endif
+constexpr int kExactColsPerWave = RT_EXACT_COLS_PER_WAVE;
+// LDS (round 5): the whole node array staged in the block's LDS when it fits (n_nodes records; the
+// launch sizes the dynamic LDS). Tier A runs one lane per column, so few waves hold the GPU and each
+// dependent node read's latency is the lane's own time: from L2 it cost the Cornell box ~10x the
+// 16-thread CPU oracle's time.
+template <unsigned F, bool LDS = false>
+__global__ void __launch_bounds__(RT_BLOCK) render_exact(RenderArgs A, int n_nodes) {
   __shared__ int stk_mem[RT_STACK * RT_BLOCK];
   int* stk = &stk_mem[threadIdx.x];
   // Tier A reproduces the reference's stream exactly, exact ties included: walk the caller's tree.
   Scene S = A.S;
   S.world = S.world_ref;
-  const int x = blockIdx.x * RT_BLOCK + threadIdx.x;
-  if (x >= A.W) return;
+  if constexpr (LDS) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_nodes[];
+    const uint4* src = reinterpret_cast<const uint4*>(A.S.nodes);
+    uint4* dst = reinterpret_cast<uint4*>(lds_nodes);
+    const int n16 = n_nodes * (int)(sizeof(rt_node) / 16);
+    for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+    S.nodes = reinterpret_cast<const rt_node*>(lds_nodes);
+  }
+  // One column per wave, on its lane 0: a column is one serial chain of draws (the stream threads every
+  // row, sample and bounce), so a wave of 64 columns ran every sample at its slowest lane's path length
+  // and through every lane's branches; alone, a lane runs only its own (RT_EXACT_COLS_PER_WAVE).
+  const int x = blockIdx.x * (RT_BLOCK / 64) * kExactColsPerWave + (int)(threadIdx.x >> 6) * kExactColsPerWave +
+                (int)(threadIdx.x & 63);
+  if ((int)(threadIdx.x & 63) >= kExactColsPerWave || x >= A.W) return;
   RngExactT<kSL<F>> g{A.gens[2 * x], A.gens[2 * x + 1]};
   const bool traced = A.trace && x == A.trace_col;
   int tn = 0;

@@ -230,14 +230,36 @@ bool env_off(const char* name) {
   const char* e = std::getenv(name);
   return e && e[0] == '0';
 }
-const void* exact_variant(unsigned f, bool shared_libm) {
+template <bool LDS>
+const void* exact_variant_l(unsigned f, bool shared_libm) {
   switch (variant_for(f)) {
     case kVarSpheres:
-      return shared_libm ? (const void*)render_exact<kVarSpheres | F_SLIBM> : (const void*)render_exact<kVarSpheres>;
+      return shared_libm ? (const void*)render_exact<kVarSpheres | F_SLIBM, LDS> : (const void*)render_exact<kVarSpheres, LDS>;
     case kVarCornell:
-      return shared_libm ? (const void*)render_exact<kVarCornell | F_SLIBM> : (const void*)render_exact<kVarCornell>;
-    default: return shared_libm ? (const void*)render_exact<F_ALL | F_SLIBM> : (const void*)render_exact<F_ALL>;
+      return shared_libm ? (const void*)render_exact<kVarCornell | F_SLIBM, LDS> : (const void*)render_exact<kVarCornell, LDS>;
+    default: return shared_libm ? (const void*)render_exact<F_ALL | F_SLIBM, LDS> : (const void*)render_exact<F_ALL, LDS>;
   }
+}
+// Blocks of the tier-A kernel: kExactColsPerWave columns per wave, RT_BLOCK / 64 waves per block.
+unsigned exact_blocks(int width) {
+  const int per_block = (RT_BLOCK / 64) * kExactColsPerWave;
+  return (unsigned)((width + per_block - 1) / per_block);
+}
+// The tier-A kernel for the ctx's scene and its dynamic LDS bytes: the node array staged in LDS when it
+// fits beside the static lane stacks (RTAMD_EXACT_LDS=0: never).
+int exact_launch(rt_ctx* c, bool shared_libm, const void** fn, size_t* bytes) {
+  const size_t need = (size_t)c->n_nodes * sizeof(rt_node);
+  const size_t budget = 160 * 1024 - (size_t)RT_STACK * RT_BLOCK * sizeof(int);
+  const char* e = std::getenv("RTAMD_EXACT_LDS");
+  if (need <= budget && !(e && e[0] == '0')) {
+    *fn = exact_variant_l<true>(c->features, shared_libm);
+    *bytes = need;
+    HIPCHK(hipFuncSetAttribute(*fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
+  } else {
+    *fn = exact_variant_l<false>(c->features, shared_libm);
+    *bytes = 0;
+  }
+  return RT_OK;
 }
 
 int launch_combine(rt_ctx* c, const RenderArgs& A, hipStream_t st) {
@@ -924,10 +946,13 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, cons
     A.gens = d_gens;
     A.out_rgb = d_img;
     A.out_lin = d_img_lin;
+    const void* fn = nullptr;
+    size_t lds = 0;
+    if (int rc = exact_launch(c, (p.flags & RT_FLAG_SHARED_LIBM) != 0, &fn, &lds)) return rc;
+    int n_nodes = c->n_nodes;
     HIPCHK(hipEventRecord(c->ev0, st));
-    void* args[] = {&A};
-    HIPCHK(hipLaunchKernel(exact_variant(c->features, (p.flags & RT_FLAG_SHARED_LIBM) != 0), dim3((p.width + RT_BLOCK - 1) / RT_BLOCK), dim3(RT_BLOCK),
-                           args, 0, st));
+    void* args[] = {&A, &n_nodes};
+    HIPCHK(hipLaunchKernel(fn, dim3(exact_blocks(p.width)), dim3(RT_BLOCK), args, lds, st));
     HIPCHK(hipEventRecord(c->ev1, st));
     if (out_gens)
       HIPCHK(hipMemcpyAsync(out_gens, d_gens, sizeof(uint64_t) * 2 * (size_t)p.width, hipMemcpyDeviceToHost, st));
@@ -1080,9 +1105,12 @@ int rt_debug_exact_trace(rt_ctx* c, const rt_camera* cam, const rt_render_params
   A.trace_n = (int*)trn.p;
   A.trace_col = col;
   A.trace_cap = cap;
-  void* args[] = {&A};
-  HIPCHK(hipLaunchKernel(exact_variant(c->features, (p.flags & RT_FLAG_SHARED_LIBM) != 0),
-                         dim3((p.width + RT_BLOCK - 1) / RT_BLOCK), dim3(RT_BLOCK), args, 0, c->stream));
+  const void* fn = nullptr;
+  size_t lds = 0;
+  if (int rc = exact_launch(c, (p.flags & RT_FLAG_SHARED_LIBM) != 0, &fn, &lds)) return rc;
+  int n_nodes = c->n_nodes;
+  void* args[] = {&A, &n_nodes};
+  HIPCHK(hipLaunchKernel(fn, dim3(exact_blocks(p.width)), dim3(RT_BLOCK), args, lds, c->stream));
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipMemcpy(out_n, trn.p, sizeof(int), hipMemcpyDeviceToHost));
