@@ -113,7 +113,7 @@ def default_selection(args):
     """True when this run launches the default kernel selection of its config (no RTAMD_* knobs, no
     culling / BVH / spp / tile overrides): only then does a committed PMC summary describe it."""
     return not any(k.startswith("RTAMD_") for k in os.environ) and not (
-        args.nan_cull or args.reference_cull or args.reference_bvh or args.spp or args.tile != 16)
+        args.nan_cull or args.reference_cull or args.reference_bvh or args.spp or args.tile != 8)
 
 
 def _pmc_summary(args):
@@ -303,7 +303,7 @@ def main():
     ap.add_argument("--reference-bvh", action="store_true",
                     help="traverse the reference's makeBVH world tree (default: SAH rebuild over the same leaves)")
     ap.add_argument("--spp", type=int, default=0, help="override spp (sampled runs of the big configs; not the metric)")
-    ap.add_argument("--tile", type=int, default=16)
+    ap.add_argument("--tile", type=int, default=8)
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (default: the affinity CPU count, capped by OMP_NUM_THREADS)")
     ap.add_argument("--cpu-spp", type=int, default=0,

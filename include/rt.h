@@ -240,7 +240,7 @@ typedef struct rt_render_params {
     int32_t rng_mode;  /* RT_RNG_EXACT | RT_RNG_PHILOX */
     uint32_t flags;
     uint64_t seed;       /* tier B Philox key */
-    int32_t tile;        /* tile edge in pixels for sharding: a multiple of 8 in [8, 256] (0 = default 16) */
+    int32_t tile;        /* tile edge in pixels for sharding: a multiple of 8 in [8, 256] (0 = default 8) */
     int32_t shard_rank;  /* this shard (0-based) */
     int32_t shard_count; /* number of shards (GPUs); tiles are dealt round-robin */
     int32_t _pad;

@@ -363,7 +363,7 @@ withCamera :: Camera -> (Ptr CameraRec -> IO a) -> IO a
 withCamera (Camera o llc horiz vert u v w lensRadius t0 t1) k =
   withArray (concatMap v3 [o, llc, horiz, vert, u, v, w] ++ [lensRadius, t0, t1]) (k . castPtr)
 
--- | rt_render_params (48 bytes); whole image (shard 0 of 1), default 16-pixel tiles.
+-- | rt_render_params (48 bytes); whole image (shard 0 of 1), default 8-pixel tiles.
 withParams :: Int -> Int -> Int -> Int -> Int32 -> Word64 -> (Ptr RenderParams -> IO a) -> IO a
 withParams w h ns maxDepth rng seed k =
   allocaBytes 48 $ \p -> do
@@ -372,7 +372,7 @@ withParams w h ns maxDepth rng seed k =
     pokeByteOff p 16 rng
     pokeByteOff p 20 (0 :: Word32)   -- flags
     pokeByteOff p 24 seed
-    pokeByteOff p 32 (16 :: Int32)   -- tile
+    pokeByteOff p 32 (8 :: Int32)    -- tile
     pokeByteOff p 36 (0 :: Int32)    -- shard_rank
     pokeByteOff p 40 (1 :: Int32)    -- shard_count
     k (castPtr p)

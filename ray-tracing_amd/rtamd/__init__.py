@@ -494,7 +494,7 @@ def mkRenderStaticEnv(scene, camera, size, ns, max_depth, n_threads=1) -> Render
     return RenderStaticEnv(scene, camera, tuple(size), int(ns), int(max_depth), int(n_threads))
 
 
-def make_params(width, height, spp, max_depth, rng_mode=RT_RNG_PHILOX, seed=1024, flags=0, tile=16,
+def make_params(width, height, spp, max_depth, rng_mode=RT_RNG_PHILOX, seed=1024, flags=0, tile=8,
                 shard_rank=0, shard_count=1) -> rt_render_params:
     p = rt_render_params()
     p.width, p.height, p.spp, p.max_depth = width, height, spp, max_depth
@@ -759,7 +759,7 @@ def shard_pixel_map(params: rt_render_params) -> np.ndarray:
     """Slab work index -> image pixel index (row * W + x) or -1 for padding, for one shard.
     Host restatement of the kernel's work_pixel() mapping (tile-major, 8x8 blocks per tile)."""
     tt, per_shard, slab = shard_geometry(params)
-    tile = params.tile or 16
+    tile = params.tile or 8
     shards = max(1, params.shard_count)
     tiles_x = (params.width + tile - 1) // tile
     w = np.arange(slab, dtype=np.int64)

@@ -93,16 +93,16 @@ def test_more_shards_than_tiles(gpu_ctx):
     sc, _ = rtamd.make_scene("three_spheres", rtamd.randGen(1024))
     cam = rtamd.camera("random_scene", 20, 20)
     gpu_ctx.upload(sc)
-    base = rtamd.make_params(20, 20, 4, 10, rtamd.RT_RNG_PHILOX, seed=4)
+    base = rtamd.make_params(20, 20, 4, 10, rtamd.RT_RNG_PHILOX, seed=4, tile=16)
     ref, _, _ = gpu_ctx.render(cam, base)
     shards = 6
-    _, _, slab = rtamd.shard_geometry(rtamd.make_params(20, 20, 4, 10, shard_count=shards))
+    _, _, slab = rtamd.shard_geometry(rtamd.make_params(20, 20, 4, 10, shard_count=shards, tile=16))
     slabs = torch.zeros((shards, slab, 3), dtype=torch.uint8, device="cuda")
     for r in range(shards):
-        p = rtamd.make_params(20, 20, 4, 10, rtamd.RT_RNG_PHILOX, seed=4, shard_rank=r, shard_count=shards)
+        p = rtamd.make_params(20, 20, 4, 10, rtamd.RT_RNG_PHILOX, seed=4, shard_rank=r, shard_count=shards, tile=16)
         gpu_ctx.render_shard_async(cam, p, slabs[r].data_ptr())
     torch.cuda.synchronize()
     img = torch.zeros((20, 20, 3), dtype=torch.uint8, device="cuda")
-    gpu_ctx.assemble_async(rtamd.make_params(20, 20, 4, 10, shard_count=shards), slabs.data_ptr(), img.data_ptr())
+    gpu_ctx.assemble_async(rtamd.make_params(20, 20, 4, 10, shard_count=shards, tile=16), slabs.data_ptr(), img.data_ptr())
     torch.cuda.synchronize()
     assert np.array_equal(img.cpu().numpy(), ref)
