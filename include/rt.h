@@ -524,6 +524,9 @@ int rt_debug_closest_hits(rt_ctx* ctx, const double* rays, int n, double tmin, d
  *   RT_PROBE_HTBL_PDF     htblPdfValue on the lights tree (src/Lib.hs:673-705): origin3, v3 -> pdf, words
  *   RT_PROBE_TEXTURE      textureValue (src/Lib.hs:496-513): texture id, u, v, p3 -> albedo3
  *   RT_PROBE_GET_RAY      getRay with `cam` (src/Lib.hs:1253-1267): s, t -> ray o3 d3 tm, words
+ *   RT_PROBE_BOX          the BVH box test: box min3 max3, ray o3 d3, t_min, t_max (14) -> the default test
+ *                         as the walks run it (division-free, rt_trace.h box_hit), the same test with
+ *                         divisions, the reference's per-axis boxRayIntersect (src/Lib.hs:798-814) (3; 1 = hit)
  */
 /*
  * Debug / parity entry: tier A (RT_RNG_EXACT) over the whole frame, with column `col`'s path segments
@@ -541,6 +544,7 @@ int rt_debug_exact_trace(rt_ctx* ctx, const rt_camera* cam, const rt_render_para
 #define RT_PROBE_HTBL_PDF 2
 #define RT_PROBE_TEXTURE 3
 #define RT_PROBE_GET_RAY 4
+#define RT_PROBE_BOX 5
 int rt_debug_probe(rt_ctx* ctx, const rt_camera* cam, int op, const double* in, int n, uint64_t seed, double* out);
 
 /*

@@ -115,11 +115,13 @@ __device__ __forceinline__ RayX prep(const Ray& r) {
   return x;
 }
 __device__ __forceinline__ Ray plain(const RayX& x) { return Ray{x.o, x.d, x.tm}; }
-// The division-free box test's condition (box_hit): a finite origin (|o| <= 2^900) and every direction
-// component either zero or in [2^-900, 2^900].
+// The division-free box test's condition (box_hit): a finite origin (|o| <= 2^100) and every direction
+// component either zero or in [2^-900, 2^900]. With the world's finite box coordinates within 2^100 (else
+// the host walks it with the per-axis test, rt_render.hip far_boxes) no slab product (f - o) * RN(1/d)
+// then overflows (|f - o| < 2^101, |RN(1/d)| <= 2^900): an infinite product is a zero axis's exact quotient.
 __device__ __forceinline__ bool ray_safe(const RayX& r) {
   return ((r.d.x == 0.0) | div_ok(r.d.x)) & ((r.d.y == 0.0) | div_ok(r.d.y)) & ((r.d.z == 0.0) | div_ok(r.d.z)) &
-         (fabs(r.o.x) <= 0x1p900) & (fabs(r.o.y) <= 0x1p900) & (fabs(r.o.z) <= 0x1p900);
+         (fabs(r.o.x) <= 0x1p100) & (fabs(r.o.y) <= 0x1p100) & (fabs(r.o.z) <= 0x1p100);
 }
 // a / d exactly, given y = RN(1/d): a zero divisor gives a * y (= the IEEE a / +-0: +-inf with the
 // sign of a xor d, NaN for a = 0 or NaN), operands and quotient in [2^-900, 2^900] the Markstein

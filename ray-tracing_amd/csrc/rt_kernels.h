@@ -827,7 +827,7 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
 // The hot-path functions one at a time on device inputs (rt_debug_probe; layouts in rt.h and
 // oracle/oracle.c oracle_probe): record i draws from its own tier-B Philox stream (key = seed, pid = i,
 // sample 0), so the oracle's golden vectors consume the same numbers.
-constexpr int kProbeIn[5] = {18, 3, 6, 6, 2}, kProbeOut[5] = {14, 4, 2, 3, 8};
+constexpr int kProbeIn[6] = {18, 3, 6, 6, 2, 14}, kProbeOut[6] = {14, 4, 2, 3, 8, 3};
 template <unsigned F>
 __global__ void __launch_bounds__(RT_BLOCK) fn_probe(Scene S, rt_camera cam, int op, const double* in, int n,
                                                     uint64_t seed, double* out) {
@@ -875,6 +875,11 @@ __global__ void __launch_bounds__(RT_BLOCK) fn_probe(Scene S, rt_camera cam, int
   } else if (op == 3) {  // textureValue
     const V3 a = texture_value<F>(S, (int)q[0], q[1], q[2], v3(q[3], q[4], q[5]));
     o[0] = a.x, o[1] = a.y, o[2] = a.z;
+  } else if (op == 5) {  // the box test: division-free (the walks'), with divisions, the reference's per-axis
+    const RayX r = prep(Ray{v3(q[6], q[7], q[8]), v3(q[9], q[10], q[11]), 0.0});
+    o[0] = box_hit(q, r, q[12], q[13], true);
+    o[1] = box_hit_exact(q, r, q[12], q[13], true);
+    o[2] = box_hit_exact(q, r, q[12], q[13], false);
   } else {  // getRay
     const Ray r = get_ray(cam, q[0], q[1], g);
     o[0] = r.o.x, o[1] = r.o.y, o[2] = r.o.z;

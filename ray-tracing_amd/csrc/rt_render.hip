@@ -60,6 +60,7 @@ struct rt_ctx {
   int n_wnodes = 0;
   int wide_stack_need = 0;
   bool rebuilt_bvh = false;
+  bool far_boxes = false;    // a BVH box coordinate beyond 2^100: the walks take the per-axis box test (cull())
   bool mixed_wide = false;   // media / frame world with 4-wide trees over its re-bounded subtrees (F_MIXW)
   bool replace_ok = false;  // frames nest <= RT_MAX_FRAMES deep: the replacement loop applies
   bool has_scene = false;
@@ -276,6 +277,9 @@ int launch_combine(rt_ctx* c, const RenderArgs& A, hipStream_t st) {
   return RT_OK;
 }
 
+// The launch's culling flags: the caller's, with the per-axis test alone for far-box worlds (rt_ctx::far_boxes).
+uint32_t cull(const rt_ctx* c, uint32_t flags) { return flags | (c->far_boxes ? RT_FLAG_REFERENCE_CULL : 0u); }
+
 int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int rank, int shards, uint8_t* d_rgb,
                   double* d_lin, hipStream_t st, unsigned long long* d_work = nullptr,
                   unsigned long long* d_prof = nullptr) {
@@ -286,7 +290,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   A.H = p->height;
   A.spp = p->spp;
   A.max_depth = p->max_depth;
-  A.flags = p->flags;
+  A.flags = cull(c, p->flags);
   long long tiles_total, per_shard, slab;
   geometry(p, A.tile, A.tiles_x, tiles_total, per_shard, slab);
   A.tiles_total = (int)tiles_total;
@@ -451,7 +455,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   const char* wenv = std::getenv("RTAMD_WIDE");
   const bool want_wide = wenv ? wenv[0] != '0' : c->rebuilt_bvh;
   // (the full variant has no 4-wide instantiation: its media-free worlds walk the binary tree)
-  const bool wide = replace && c->d_wnodes && !(p->flags & RT_FLAG_REFERENCE_CULL) && want_wide && !is_full(var);
+  const bool wide = replace && c->d_wnodes && !(A.flags & RT_FLAG_REFERENCE_CULL) && want_wide && !is_full(var);
   const int loop = wide ? 2 : (replace ? 1 : 0);
   if (loop && is_full(var)) {  // (kTail kernels; the per-sample loop claims whole work-items)
     const char* te = std::getenv("RTAMD_TAIL");
@@ -800,6 +804,14 @@ int upload_prepared(rt_ctx* c, const rt::PreparedScene& P, const rt_scene_desc* 
   c->stack_need = P.stack_need;
   c->wide_stack_need = P.wide_stack_need;
   c->rebuilt_bvh = P.rebuilt_bvh;
+  // The division-free box test (rt_trace.h box_hit) reads an infinite slab product as the quotient; with
+  // |origin| <= 2^100 (ray_safe) and |d| >= 2^-900 that holds while every finite box coordinate is within
+  // 2^100 (no finite quotient overflows as a product). Worlds beyond it are walked with the reference's
+  // per-axis test alone (RT_FLAG_REFERENCE_CULL), which divides.
+  c->far_boxes = false;
+  for (const rt_node& x : P.nodes)
+    if ((x.type & RT_TYPE_MASK) == RT_NODE_BVH)
+      for (int k = 0; k < 6; ++k) c->far_boxes |= std::isfinite(x.f[k]) && std::fabs(x.f[k]) > 0x1p100;
   c->mixed_wide = P.mixed_wide;
   c->replace_ok = P.replace_ok;
   c->has_scene = true;
@@ -946,7 +958,7 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, cons
     A.H = p.height;
     A.spp = p.spp;
     A.max_depth = p.max_depth;
-    A.flags = p.flags;  // (RT_FLAG_REFERENCE_CULL)
+    A.flags = cull(c, p.flags);  // (RT_FLAG_REFERENCE_CULL)
     A.gens = d_gens;
     A.out_rgb = d_img;
     A.out_lin = d_img_lin;
@@ -1053,7 +1065,7 @@ int rt_debug_closest_hits(rt_ctx* c, const double* rays, int n, double tmin, dou
   double* d_rays = (double*)rays_buf.p;
   double* d_out = (double*)out_buf.p;
   HIPCHK(hipMemcpy(d_rays, rays, sizeof(double) * 7 * (size_t)n, hipMemcpyHostToDevice));
-  const int joint = !(flags & RT_FLAG_REFERENCE_CULL);
+  const int joint = !(cull(c, flags) & RT_FLAG_REFERENCE_CULL);
   const dim3 grid((n + RT_BLOCK - 1) / RT_BLOCK);
   if ((flags & RT_DEBUG_QNODE) && !c->d_qnodes)
     return unsupported("rt_debug_closest_hits: no quantised 4-wide tree for this world (spheres-only worlds)");
@@ -1102,7 +1114,7 @@ int rt_debug_exact_trace(rt_ctx* c, const rt_camera* cam, const rt_render_params
   A.H = p.height;
   A.spp = p.spp;
   A.max_depth = p.max_depth;
-  A.flags = p.flags;
+  A.flags = cull(c, p.flags);
   A.gens = (uint64_t*)gens.p;
   A.out_rgb = (uint8_t*)img.p;
   A.trace = (double*)tr.p;
@@ -1123,7 +1135,7 @@ int rt_debug_exact_trace(rt_ctx* c, const rt_camera* cam, const rt_render_params
 }
 
 int rt_debug_probe(rt_ctx* c, const rt_camera* cam, int op, const double* in, int n, uint64_t seed, double* out) {
-  if (!c || !in || !out || n < 0 || op < 0 || op > 4 || (op == 4 && !cam)) return invalid("rt_debug_probe: bad argument");
+  if (!c || !in || !out || n < 0 || op < 0 || op > RT_PROBE_BOX || (op == 4 && !cam)) return invalid("rt_debug_probe: bad argument");
   if (!c->has_scene) {
     rt::set_error("rt_debug_probe: no scene uploaded");
     return RT_E_STATE;

@@ -129,7 +129,7 @@ __device__ __forceinline__ bool box_hit_exact(const double* f, const RayX& r, do
 // The default (joint) test decided without divisions. When every quotient is finite and
 // non-NaN, (reference per-axis test) AND (joint test) is exactly L < U with
 // L = max(t_min, min(ta,tb) over axes) and U = min(t_max, max(ta,tb) over axes), and L and U are
-// each one of the exact quotients (or t_min / t_max). For a `safe` ray (finite origin, every
+// each one of the exact quotients (or t_min / t_max). For a `safe` ray (|o| <= 2^100, every
 // non-zero |d| in [2^-900, 2^900] so y = RN(1/d) is normal) q' = n * y is within 2^-51 |q| + 2^-1074 of
 // q = RN(n / d), so L', U' are within 2^-50 (|L'| + |U'|) + 2^-1073 of L, U: outside the band
 // U' - L' in [-b, b], b = 2^-48 (|L'| + |U'|) (> 2^-1000 whenever the decision is taken), the
@@ -137,8 +137,11 @@ __device__ __forceinline__ bool box_hit_exact(const double* f, const RayX& r, do
 // quotient (+-inf): with the origin inside that slab (-inf, +inf) it does not constrain L or U, as it
 // constrains nothing in the reference's per-axis test (t0 = -inf, t1 = +inf); outside it both are +inf
 // (or both -inf), so L = +inf (or U = -inf) — and the reference's test of that axis fails (its tmin is
-// +inf, or its tmax -inf). NaN quotients (n = 0: the origin on a slab plane of a zero axis), overflowed
-// or banded cases fall through to the exact test. Branch-free except for that (rare) fall-through.
+// +inf, or its tmax -inf). No other product is infinite: the host walks a world with a finite box
+// coordinate beyond 2^100 with the per-axis test instead (rt_render.hip far_boxes), so |n| < 2^101 and
+// |n * y| < 2^1001 (an overflowed product of a finite quotient must not read as +-inf). NaN
+// quotients (n = 0: the origin on a slab plane of a zero axis) or banded cases fall through to the exact
+// test. Branch-free except for that (rare) fall-through.
 __device__ __forceinline__ bool box_hit(const double* f, const RayX& r, double t_min, double t_max, bool joint) {
   if (!joint) return box_hit_exact(f, r, t_min, t_max, false);
   double L = t_min, U = t_max;

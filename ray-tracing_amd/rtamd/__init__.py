@@ -44,9 +44,9 @@ MATH_OPS = {"div": 0, "div_exact": 1, "sqrt": 2, "sin": 3, "cos": 4, "atan": 5, 
             "sl_log": 16, "sl_ghc_atan2": 17}  # sl_*: include/rt_libm.h (RT_FLAG_SHARED_LIBM)
 
 # rt_debug_probe / oracle_probe: function -> op id, doubles per input / output record (rt.h)
-PROBES = {"scatter": 0, "htbl_random": 1, "htbl_pdf": 2, "texture": 3, "get_ray": 4}
-PROBE_IN = (18, 3, 6, 6, 2)
-PROBE_OUT = (14, 4, 2, 3, 8)
+PROBES = {"scatter": 0, "htbl_random": 1, "htbl_pdf": 2, "texture": 3, "get_ray": 4, "box": 5}
+PROBE_IN = (18, 3, 6, 6, 2, 14)
+PROBE_OUT = (14, 4, 2, 3, 8, 3)
 
 XYPlane, XZPlane, YZPlane = 0, 1, 2
 XAxis, YAxis, ZAxis = 0, 1, 2

@@ -44,7 +44,7 @@ def fast(lo, hi, o, d, t_min, t_max):
         safe = np.ones(len(o), dtype=bool)
         for a in range(3):
             safe &= (d[:, a] == 0.0) | in_range(d[:, a])
-            safe &= np.abs(o[:, a]) <= 2.0 ** 900
+            safe &= np.abs(o[:, a]) <= 2.0 ** 100
         L, U = t_min.copy(), t_max.copy()
         nan = np.zeros(len(o), dtype=bool)
         for a in range(3):
@@ -104,3 +104,25 @@ def test_quirk_direction_is_decided_without_divisions():
     dec, ans = fast(lo, hi, o, d, t_min, t_max)
     assert dec.mean() > 0.999
     assert (ans[dec] == exact(lo, hi, o, d, t_min, t_max)[dec]).all()
+
+
+def test_far_boxes_are_left_to_the_per_axis_test():
+    """Why the host walks a world with a finite box coordinate beyond 2^100 with the per-axis test
+    (rt_render.hip far_boxes): there a slab product can overflow while the quotient is finite, and the
+    fast path would read the product's +inf as the quotient (a false reject). Within 2^100
+    (and |o| <= 2^100, ray_safe) a product over a non-zero axis stays below 2^1001."""
+    import test_box_probe as bp
+    r = bp.overflow_records(8)
+    lo, hi, o, d, t_min, t_max = r[:, 0:3], r[:, 3:6], r[:, 6:9], r[:, 9:12], r[:, 12], r[:, 13]
+    dec, ans = fast(lo, hi, o, d, t_min, t_max)
+    assert (dec & ~ans).all() and exact(lo, hi, o, d, t_min, t_max).all()
+    rng = np.random.default_rng(9)
+    n = 200_000
+    lo = rng.uniform(-1, 1, (n, 3)) * 2.0 ** 100
+    hi = np.minimum(lo + rng.uniform(0, 2, (n, 3)) * 2.0 ** 99, 2.0 ** 100)
+    o = rng.uniform(-1, 1, (n, 3)) * 2.0 ** 100
+    d = rng.choice([-1.0, 1.0], (n, 3)) * 2.0 ** -900 * rng.uniform(1, 1.001, (n, 3))
+    with np.errstate(over="ignore"):
+        assert np.isfinite((lo - o) * (1.0 / d)).all() and np.isfinite((hi - o) * (1.0 / d)).all()
+    dec, ans = fast(lo, hi, o, d, np.full(n, 1e-4), np.full(n, np.inf))
+    assert (ans[dec] == exact(lo, hi, o, d, np.full(n, 1e-4), np.full(n, np.inf))[dec]).all()
