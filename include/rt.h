@@ -218,7 +218,8 @@ static inline int rt_sample_chunk(int64_t pixels, int spp) {
                                Output-identical; off by default. */
 #define RT_FLAG_REFERENCE_CULL 2u /* cull BVH boxes with the reference's per-axis test only
                                (src/Lib.hs:798-814). Default: that test AND the joint slab test,
-                               which only prunes boxes that cannot hold a hit. */
+                               which only prunes boxes that cannot hold a hit. A world
+                               with a finite BVH box coordinate beyond 2^100 always takes this flag. */
 #define RT_FLAG_NAN_ZERO 4u /* tier B, parity diagnostic (NOT the reference's semantics): a sample
                                contribution channel that is NaN is added as 0, so that the finite
                                part of every sample reaches the average. The reference's Lambertian
