@@ -220,12 +220,13 @@ static inline int rt_sample_chunk(int64_t pixels, int spp) {
                                (src/Lib.hs:798-814). Default: that test AND the joint slab test,
                                which only prunes boxes that cannot hold a hit. A world
                                with a finite BVH box coordinate beyond 2^100 always takes this flag. */
-#define RT_FLAG_NAN_ZERO 4u /* tier B, parity diagnostic (NOT the reference's semantics): a sample
+#define RT_FLAG_NAN_ZERO 4u /* tiers A and B, parity diagnostic (NOT the reference's semantics): a sample
                                contribution channel that is NaN is added as 0, so that the finite
                                part of every sample reaches the average. The reference's Lambertian
                                light-mixture quirk makes most pixels of the bench frames NaN (C2 mid
                                rows, all of C4 at 1000 spp); with this flag the same launches carry
-                               every sample's finite colour to a comparable output. */
+                               every sample's finite colour to a comparable output (and tier A's and
+                               tier B's finite parts can be compared as distributions). */
 #define RT_FLAG_SHARED_LIBM 8u /* tier A only, parity aid: sin, cos, log, atan, asin (and x ** 5) from the
                                portable include/rt_libm.h instead of the device's OCML, the functions the
                                oracle evaluates in the same mode. A column's tier-A stream is one serial
@@ -365,10 +366,12 @@ int rt_ctx_devices(const rt_ctx* ctx, int* out_n, int* out_devices, int cap);
  * kernel_ms[r] = device r's render launches (chunk batches included), gather_ms = from the first
  * device's render end to the end of the RCCL gather on its stream (includes waiting for the slowest
  * device), assemble_ms = the assemble kernel, frame_ms = first launch to assembled image (before the
- * device-to-host copy). n_devices = 1 and gather_ms = 0 on a one-device ctx. */
+ * device-to-host copy). n_devices = 1 and gather_ms = 0 on a one-device ctx. device_allocs = device
+ * allocations (hipMalloc) the call made over all the ctx's devices: the ctx keeps its frame buffers (slabs,
+ * gathered slabs, image, chunk sums) and grows them on demand, so a repeated frame of one size makes none. */
 typedef struct rt_frame_timing {
     int32_t n_devices;
-    int32_t _pad;
+    int32_t device_allocs;
     double kernel_ms[RT_MAX_DEVICES];
     double gather_ms;
     double assemble_ms;

@@ -10,9 +10,10 @@
 --
 -- UNTESTED AS HASKELL: no GHC exists in the build image or on the GPU box (SURVEY.md §0.2), so this
 -- file has never been compiled. Its call sequence — post-order flattening of the Hittable tree into
--- an rt_scene_desc, rt_create_multi over every visible GPU (rt_device_count), rt_upload_scene,
--- rt_render (tier A, one SplitMix generator per column; tier B tile-sharded over the GPUs and gathered
--- with RCCL inside librtamd), rows split top first, rt_destroy — is mirrored in C by
+-- an rt_scene_desc, rt_create on GPU 0 (or, opt-in for tier B, rt_create_multi over n GPUs),
+-- rt_upload_scene, rt_render (tier A, one SplitMix generator per column; tier B one Philox stream per
+-- pixel and sample, tile-sharded over the GPUs and gathered with RCCL inside librtamd on a multi-GPU
+-- ctx), rows split top first, rt_destroy — is mirrored in C by
 -- tests/c/ffi_sequence.c, which tests/test_ffi_sequence.py compiles and runs (the rendering half on the
 -- GPU, checked against the CPU oracle on the same flattened records).
 --
@@ -33,6 +34,7 @@ module RenderAMD
   ( -- * Drop-ins for runRender
     runRenderAMD
   , runRenderAMDPhilox
+  , runRenderAMDPhiloxOn
     -- * The flattened scene (include/rt.h records)
   , FlatScene (..)
   , RtNode (..)
@@ -70,7 +72,11 @@ data RenderParams  -- rt_render_params, 48 bytes
 
 foreign import ccall unsafe "rt.h rt_device_count"
   c_rt_device_count :: Ptr CInt -> IO CInt
+-- one ctx on one GPU (the default: runRenderAMD, runRenderAMDPhilox)
+foreign import ccall unsafe "rt.h rt_create"
+  c_rt_create :: CInt -> Ptr (Ptr RtCtx) -> IO CInt
 -- one ctx over n GPUs (NULL device list = 0..n-1): tier-B frames shard over them, RCCL gathers
+-- (runRenderAMDPhiloxOn, opt-in)
 foreign import ccall unsafe "rt.h rt_create_multi"
   c_rt_create_multi :: CInt -> Ptr CInt -> Ptr (Ptr RtCtx) -> IO CInt
 foreign import ccall unsafe "rt.h rt_destroy"
@@ -382,11 +388,12 @@ withParams w h ns maxDepth rng seed k =
 columnGens :: [RandGen] -> [Word64]
 columnGens gens = concat [[s, g] | RandGen std <- gens, let (s, g) = unseedSMGen (unStdGen std)]
 
--- | Render on every visible GPU (tier B: tile shards gathered by RCCL; tier A: per-column streams do not
--- shard, the first GPU renders); the raw H x W x 3 bytes, top row first.
-renderBytes :: Scene -> Camera -> (Int, Int) -> Int -> Int -> Int32 -> Word64 -> [Word64]
+-- | Render on `gpus` GPUs (<= 1: device 0 alone, rt_create; n > 1: rt_create_multi over devices
+-- 0..n-1, at most the visible ones — tier B's tile shards gathered by RCCL; tier A's per-column streams
+-- do not shard, so a tier-A frame always renders on one GPU); the raw H x W x 3 bytes, top row first.
+renderBytes :: Int -> Scene -> Camera -> (Int, Int) -> Int -> Int -> Int32 -> Word64 -> [Word64]
             -> IO (SV.Vector Word8)
-renderBytes scene cam (w, h) ns maxDepth rng seed gensW = do
+renderBytes gpus scene cam (w, h) ns maxDepth rng seed gensW = do
   let flat = flattenScene scene
   bracket acquire c_rt_destroy $ \ctx -> do
     withSceneDesc flat $ \d -> check "rt_upload_scene" (c_rt_upload_scene ctx d)
@@ -400,8 +407,11 @@ renderBytes scene cam (w, h) ns maxDepth rng seed gensW = do
   where
     acquire = alloca $ \pn -> alloca $ \pctx -> do
       check "rt_device_count" (c_rt_device_count pn)
-      n <- peek pn
-      check "rt_create_multi" (c_rt_create_multi (min n 16) nullPtr pctx)  -- (RT_MAX_DEVICES = 16)
+      avail <- peek pn
+      let n = minimum [fromIntegral (max 1 gpus), avail, 16]  -- (RT_MAX_DEVICES = 16)
+      if n <= 1 || rng == rtRngExact
+        then check "rt_create" (c_rt_create 0 pctx)
+        else check "rt_create_multi" (c_rt_create_multi n nullPtr pctx)
       peek pctx
 
 -- | Rows of pixels, top row first, each `cols` wide.
@@ -414,9 +424,12 @@ toRows w h cols bytes =
 -- | Drop-in for @runRender (mkRenderStaticEnv scene cam (w, h) ns maxDepth _) gens@
 -- (src/Lib.hs:1491-1523): tier A, the reference's own stream layout — column x draws from gens !! x,
 -- threaded down the column through every sample and bounce — so the bytes are the reference's
--- (within the transcendental-ulp tolerance of SURVEY.md §8d). Like runRender's VV.zip
--- (src/Lib.hs:1519), a row holds min (length gens) w pixels: with fewer generators than columns the
--- rows are truncated (the missing columns are rendered with a copy of the first generator and cut).
+-- (within the transcendental-ulp tolerance of SURVEY.md §8d; DESIGN.md §4.5 gives the measured
+-- agreement with a glibc-hosted reference). It is the EXACT mode, at CPU speed: a column is one serial
+-- chain of draws, so only W lanes work (DESIGN.md §3.3); 'runRenderAMDPhilox' is the fast path. Like
+-- runRender's VV.zip (src/Lib.hs:1519), a row holds min (length gens) w pixels: with fewer generators
+-- than columns the rows are truncated (the missing columns are rendered with a copy of the first
+-- generator and cut). One GPU (rt_create 0).
 runRenderAMD :: Scene -> Camera -> (Int, Int) -> Int -> Int -> [RandGen] -> IO [VV.Vector RGB]
 runRenderAMD scene cam (w, h) ns maxDepth gens = do
   let used = take w gens
@@ -425,12 +438,19 @@ runRenderAMD scene cam (w, h) ns maxDepth gens = do
     then return (replicate (max 0 h) VV.empty)
     else do
       let padded = used ++ replicate (w - cols) (head used)
-      bytes <- renderBytes scene cam (w, h) ns maxDepth rtRngExact 0 (columnGens padded)
+      bytes <- renderBytes 1 scene cam (w, h) ns maxDepth rtRngExact 0 (columnGens padded)
       return (toRows w h cols bytes)
 
 -- | The fast path: tier B (one Philox4x32-10 stream per pixel and sample, keyed by `seed`), the
--- same image statistically (DESIGN.md §2), full width.
+-- same image statistically (DESIGN.md §2, §4.6), full width, on one GPU.
 runRenderAMDPhilox :: Scene -> Camera -> (Int, Int) -> Int -> Int -> Word64 -> IO [VV.Vector RGB]
-runRenderAMDPhilox scene cam (w, h) ns maxDepth seed = do
-  bytes <- renderBytes scene cam (w, h) ns maxDepth rtRngPhilox seed []
+runRenderAMDPhilox = runRenderAMDPhiloxOn 1
+
+-- | 'runRenderAMDPhilox' over `gpus` GPUs of the node (opt-in): the image's tiles dealt round-robin
+-- over the devices and gathered to the first with RCCL inside librtamd (rt_create_multi). The bytes
+-- equal the one-GPU render's (tier B is shard-invariant). Its N > 1 path has run only where the GPU
+-- box had one device (DESIGN.md §3.6).
+runRenderAMDPhiloxOn :: Int -> Scene -> Camera -> (Int, Int) -> Int -> Int -> Word64 -> IO [VV.Vector RGB]
+runRenderAMDPhiloxOn gpus scene cam (w, h) ns maxDepth seed = do
+  bytes <- renderBytes gpus scene cam (w, h) ns maxDepth rtRngPhilox seed []
   return (toRows w h w bytes)

@@ -725,7 +725,8 @@ static uint8_t scale_color(double x) {
 /* ------------------------------------------------------------------ runRender */
 /* One pixel, tier A: uniformRandomUVs (Lib.hs:1358-1371, list in REVERSE draw order) then
  * renderPos (Lib.hs:1343-1350: foldM sampleColor in list order, then divide by ns). */
-static V3 render_pixel_exact(const Ctx* c, int x, int y, Rng* g, double* uvbuf) {
+static V3 nan_zero(V3 a);
+static V3 render_pixel_exact(const Ctx* c, int x, int y, Rng* g, double* uvbuf, int nanz) {
     int ns = c->spp;
     for (int i = 0; i < ns; ++i) {
         double ru = D(g), rv = D(g);
@@ -737,6 +738,7 @@ static V3 render_pixel_exact(const Ctx* c, int x, int y, Rng* g, double* uvbuf) 
         g_tr_j = ns - 1 - i;
         Ray r = get_ray(c, uvbuf[2 * i], uvbuf[2 * i + 1], g);
         V3 c1 = ray_color(c, r, c->max_depth, g);
+        if (nanz) c1 = nan_zero(c1); /* RT_FLAG_NAN_ZERO (tiers A and B: the tier-A/B statistical tests) */
         acc = vadd(acc, c1);
         CNT(c, C_SAMPLES);
     }
@@ -825,7 +827,7 @@ int oracle_render_rows(const rt_scene_desc* scene, const rt_camera* cam, const r
                 g.draws = counters ? &cnt[C_DRAWS] : NULL;
                 for (int row = 0; row < row1; ++row) {
                     int y = H - 1 - row;
-                    V3 a = render_pixel_exact(&c, x, y, &g, uvbuf);
+                    V3 a = render_pixel_exact(&c, x, y, &g, uvbuf, (p->flags & RT_FLAG_NAN_ZERO) != 0);
                     store_pixel(rgb, linear, (int64_t)row * W + x, a);
                 }
                 if (out_gens) { out_gens[2 * x] = g.seed; out_gens[2 * x + 1] = g.gamma; }
@@ -879,7 +881,7 @@ int oracle_exact_trace(const rt_scene_desc* scene, const rt_camera* cam, const r
     g_tr = out; g_tr_n = 0; g_tr_cap = cap;
     for (int row = 0; row < p->height; ++row) {
         g_tr_row = row;
-        (void)render_pixel_exact(&c, col, p->height - 1 - row, &g, uvbuf);
+        (void)render_pixel_exact(&c, col, p->height - 1 - row, &g, uvbuf, (p->flags & RT_FLAG_NAN_ZERO) != 0);
     }
     *out_n = g_tr_n;
     g_tr = NULL;

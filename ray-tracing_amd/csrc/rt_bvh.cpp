@@ -646,8 +646,11 @@ bool build_wide_bvh(const std::vector<rt_node>& nodes, int root, std::vector<rt_
 // sub-trees), and each occurrence draws with its own key. So every record on a path to a medium is
 // copied once per path (appended, children before parents) and each medium copy carries key + 1 in
 // f[1]; media-free sub-trees stay shared. A medium already keyed (f[1] >= 1: an unfolded array uploaded
-// again) keeps its key. Returns the unfolded root (`root` itself when no medium lies below it); -1 when
-// the unfolded tree would be too large (more than 2^22 records) or is not a DAG with children first.
+// again) keeps its key — only when every occurrence is keyed, each by a distinct integer key below 2^31
+// (a keyed record reached along two paths, or a caller's key equal to an unkeyed occurrence's
+// rank, would make two occurrences draw the same numbers). Returns the unfolded root (`root` itself when
+// no medium lies below it); -1 when the unfolded tree would be too large (more than 2^22 records) or is
+// not a DAG with children first; -2 when the keys break that rule.
 int unfold_media(std::vector<rt_node>& nodes, int root) {
   const int n0 = (int)nodes.size();
   if (root < 0 || root >= n0) return -1;
@@ -668,7 +671,9 @@ int unfold_media(std::vector<rt_node>& nodes, int root) {
     return m;
   };
   if (!has(root, 0)) return ok ? root : -1;
-  uint32_t rank = 0;
+  uint32_t rank = 0, keyed = 0;
+  bool keys_ok = true;
+  std::vector<double> keys;  // (the caller's keys, f[1] = key + 1)
   std::function<int(int)> copy = [&](int id) -> int {
     if (!ok || !has(id, 0)) return id;
     if ((int)nodes.size() >= (1 << 22)) {
@@ -677,7 +682,13 @@ int unfold_media(std::vector<rt_node>& nodes, int root) {
     }
     rt_node x = nodes[id];  // (a copy: `nodes` grows)
     if (x.type == RT_NODE_CONSTANT_MEDIUM) {
-      if (!(x.f[1] >= 1.0)) x.f[1] = (double)rank + 1.0;
+      if (x.f[1] >= 1.0) {
+        ++keyed;
+        keys_ok &= x.f[1] <= 0x1p31 && x.f[1] == std::floor(x.f[1]);
+        keys.push_back(x.f[1]);
+      } else {
+        x.f[1] = (double)rank + 1.0;
+      }
       ++rank;
     } else if (x.type == RT_NODE_BVH) {
       const int a = copy(x.a);
@@ -691,9 +702,13 @@ int unfold_media(std::vector<rt_node>& nodes, int root) {
     return (int)nodes.size() - 1;
   };
   const int r = copy(root);
-  if (!ok) {
+  if (ok && keyed) {  // keyed occurrences: all of them, with distinct keys
+    std::sort(keys.begin(), keys.end());
+    keys_ok &= keyed == rank && std::adjacent_find(keys.begin(), keys.end()) == keys.end();
+  }
+  if (!ok || !keys_ok) {
     nodes.resize(n0);
-    return -1;
+    return ok ? -2 : -1;
   }
   return r;
 }
@@ -830,7 +845,8 @@ extern "C" int rt_rebuild_bvh(const rt_scene_desc* in, rt_node* out_nodes, int c
   std::vector<rt_node> nodes(in->nodes, in->nodes + in->n_nodes);
   const int unfolded = rt::unfold_media(nodes, in->world_root);
   if (unfolded < 0) {
-    rt::set_error("rt_rebuild_bvh: the world tree is not a DAG with children first, or unfolds too large");
+    rt::set_error(unfolded == -2 ? "rt_rebuild_bvh: medium keys (f[1]) set on some occurrences only, or repeated"
+                                 : "rt_rebuild_bvh: the world tree is not a DAG with children first, or unfolds too large");
     return RT_E_INVALID;
   }
   const int root = rt::rebuild_for_device(nodes, unfolded);

@@ -754,6 +754,7 @@ __global__ void __launch_bounds__(RT_BLOCK) render_exact(RenderArgs A, int n_nod
         }
         if (end) break;
       }
+      if (A.flags & RT_FLAG_NAN_ZERO) contrib = nan_zero(contrib);
       sum = sum + contrib;
     }
     store_pixel(A, (long long)row * A.W + x, divide(sum, (double)ns));
@@ -804,6 +805,7 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
     Trav t;
     trav_begin<F>(t, r, S.world, tmin, tmax);
     if (S.ref_walk) trav_restart_ref(t, S.world, tmax);  // (the re-bounded skeleton, mixed walk)
+    trav_media_first<F>(S, t, tmin, cnt, g, side);        // (hoisted media: the render loop's walk prelude)
     bool walking = true;
     walk_until<F>(S, t, walking, tmin, stk, RT_BLOCK, joint != 0, 0, 0, cnt, g, side);
     if (t.tie || (kRefMixed<F> && t.lite)) {

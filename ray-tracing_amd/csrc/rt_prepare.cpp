@@ -303,7 +303,9 @@ void mixed_wide_trees(PreparedScene& P, const std::vector<rt_node>& host, const 
     return memo[id] = r;
   };
   const int need = need_of(world);
-  if (need + 2 > RT_WSTACK) return;  // (the binary walk's bound stays)
+  // (+ 3: the walk's 2 entries of headroom, and one more for the leaf postponement's parked next node,
+  // rt_trace.h kMixPostpone; beyond that the binary walk's bound stays)
+  if (need + 3 > RT_WSTACK) return;
   for (int r : roots) dev[r].c = RT_BVH_ORDERED | (dev[r].c & 3) | RT_WROOT | (wroot[r] << 2);
   P.wnodes = std::move(wide);
   P.leaves = std::move(leaves);
@@ -344,6 +346,9 @@ int prepare_scene(const rt_scene_desc* din, uint32_t flags, PreparedScene& P) {
   // every medium occurrence its own record, keyed (tier-B draws; rt_bvh.cpp unfold_media): the caller's
   // tree as the walks take it in the reference's order (tier A, exact-tie redos)
   const int unfolded = unfold_media(nodes, din->world_root);
+  if (unfolded == -2)
+    return fail_with(RT_E_INVALID, "rt_upload_scene: medium keys (f[1] = key + 1) must be set on every medium "
+                                   "occurrence of the world or on none, distinct integers below 2^31");
   if (unfolded < 0)
     return fail_with(RT_E_UNSUPPORTED, "rt_upload_scene: the world's medium occurrences unfold to more than 2^22 records");
   dd.world_root = unfolded;

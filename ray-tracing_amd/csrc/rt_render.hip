@@ -80,6 +80,16 @@ struct rt_ctx {
   // peers[r - 1] is device r's, comms[r] its communicator (ncclCommInitAll, ranks in list order).
   std::vector<rt_ctx*> peers;
   std::vector<ncclComm_t> comms;
+  // rt_render's own device buffers, kept between calls and grown on demand (every rt_render returns after
+  // its stream is drained, so the next call may reuse them): the slab (RGB8, fp64) this device renders
+  // into, and on a multi-device ctx's first device the gathered slabs and the assembled image; tier A's
+  // column generators. Repeated frames of one size allocate nothing.
+  struct FrameBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+  };
+  FrameBuf fb_slab, fb_slab_lin, fb_gather, fb_gather_lin, fb_img, fb_img_lin, fb_gens;
+  int allocs = 0;  // hipMalloc calls made on this device by the current rt_render (rt_frame_timing)
 };
 
 namespace {
@@ -134,6 +144,27 @@ struct DeviceGuard {
 #define DEVICE_SCOPE(dev)                                  \
   DeviceGuard _dg(dev);                                    \
   if (_dg.err != hipSuccess) return hip_fail(_dg.err, "hipSetDevice")
+
+// A frame buffer of the ctx with at least `need` bytes on the current device (the caller selects the
+// ctx's device): reused as is when large enough, else freed and allocated again (counted in c->allocs).
+int grow(rt_ctx* c, rt_ctx::FrameBuf& b, size_t need) {
+  if (need <= b.bytes) return RT_OK;
+  (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+  ++c->allocs;
+  HIPCHK(hipMalloc(&b.p, need));
+  b.bytes = need;
+  return RT_OK;
+}
+void free_frame_bufs(rt_ctx* c) {
+  for (rt_ctx::FrameBuf* b : {&c->fb_slab, &c->fb_slab_lin, &c->fb_gather, &c->fb_gather_lin, &c->fb_img,
+                              &c->fb_img_lin, &c->fb_gens}) {
+    (void)hipFree(b->p);
+    b->p = nullptr;
+    b->bytes = 0;
+  }
+}
 
 int invalid(const std::string& s) {
   rt::set_error(s);
@@ -337,6 +368,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
         (void)hipFree(c->d_partial);
         c->d_partial = nullptr;
         c->partial_bytes = 0;
+        ++c->allocs;
         HIPCHK(hipMalloc((void**)&c->d_partial, need));
         c->partial_bytes = need;
       }
@@ -344,6 +376,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
         (void)hipFree(c->d_acc);
         c->d_acc = nullptr;
         c->acc_bytes = 0;
+        ++c->allocs;
         HIPCHK(hipMalloc((void**)&c->d_acc, need_acc));
         c->acc_bytes = need_acc;
       }
@@ -370,6 +403,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
       (void)hipFree(c->d_tail);
       c->d_tail = nullptr;
       c->tail_bytes = 0;
+      ++c->allocs;
       HIPCHK(hipMalloc((void**)&c->d_tail, need_tail));
       c->tail_bytes = need_tail;
     }
@@ -467,12 +501,15 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   // variant on the replacement loop 3 (C4 at 100 spp: 90.9 vs 87.5 Msamples/s at 2), on the
   // per-sample loop 2 despite 784 B/lane of scratch (C4 35.2 vs 23.4 at 1 wave, 9.1 at 3)
   int waves = (var == kVarSpheres || loop) ? waves_target(3) : waves_target(is_full(var) ? 2 : 1);
+  // the mixed walk's leaf postponement (kMixPostpone, rt_trace.h) keeps a lane's next node on the stack
+  // while its parked leaf is tested (or its frame opened): one stack entry more
+  const int postpone = (loop == 1 && (var & F_MIXW) && RT_MIXW_POSTPONE) ? 1 : 0;
   // Side slots after the stacks, then the 4 lane ints philox_loop2 keeps in LDS (RT_LANE_LDS)
   const int side_ints = side_ints_of(var, c->scene.frames, loop) + (lane_lds_of(var, loop) ? 4 : 0);
   // LDS-staged kernel when the traversal's node array plus the stacks fit one CU's 160 KiB
   // (RTAMD_LDS=0 disables it for A/B runs).
   if (!count && !env_off("RTAMD_LDS") && (!is_full(var) || loop)) {
-    const int entries = wide ? c->wide_stack_need + 3 : c->stack_need + 2;  // (wide_node writes 3 slots)
+    const int entries = wide ? c->wide_stack_need + 3 : c->stack_need + 2 + postpone;  // (wide_node writes 3 slots)
     const int items = wide ? c->n_wnodes : c->n_nodes;
     const size_t rec = wide ? sizeof(rt_wnode) : sizeof(rt_node);
     const bool leaf_lds = wide && !env_off("RTAMD_LEAF_LDS");  // RTAMD_LEAF_LDS=0: leaves never in LDS
@@ -505,7 +542,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   // 64-byte quantised form: A/B only, measured slower)
   const void* fn = philox_kernel(var, loop, false, count ? 1 : waves, count, false, loop == 2 && c->d_qnodes);
   // replacement loops: lane stacks (+ Side slots) in dynamic LDS, sized for this world's stack bound
-  int entries = wide ? c->wide_stack_need + 3 : c->stack_need + 2;  // (wide_node writes 3 slots)
+  int entries = wide ? c->wide_stack_need + 3 : c->stack_need + 2 + postpone;  // (wide_node writes 3 slots)
   const size_t dyn = loop ? (size_t)(entries + side_ints) * RT_BLOCK * sizeof(int) : 0;
   if (loop) HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
   int bpc = 1;
@@ -520,26 +557,6 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   return run(fn, dim3(grid), dim3(RT_BLOCK), dyn, args);
 }
 
-// Device buffer on a given device (freed with that device selected).
-struct DevBufOn {
-  int dev = -1;
-  void* p = nullptr;
-  DevBufOn() = default;
-  DevBufOn(const DevBufOn&) = delete;
-  DevBufOn& operator=(const DevBufOn&) = delete;
-  ~DevBufOn() {
-    if (!p) return;
-    DeviceGuard _dg(dev);
-    (void)hipFree(p);
-  }
-  int alloc(int device, size_t bytes) {
-    dev = device;
-    DEVICE_SCOPE(device);
-    HIPCHK(hipMalloc(&p, bytes));
-    return RT_OK;
-  }
-};
-
 // rt_render, tier B, on a multi-device ctx (rt_create_multi): shard r of N = the ctx's r-th device. Every
 // device renders its tiles into a slab on its own stream (the launches are queued from this thread and
 // run concurrently); the slabs are gathered to device 0 by RCCL (one ncclGather per communicator, grouped,
@@ -553,26 +570,36 @@ int render_multi(rt_ctx* c, const rt_camera* cam, rt_render_params p, uint8_t* o
   geometry(&p, tile, tiles_x, tt, ps, slab);
   auto dev_ctx = [&](int r) { return r == 0 ? c : c->peers[r - 1]; };
   const long long npx = (long long)p.width * p.height;
-  std::vector<DevBufOn> send(n), send_lin(n);
-  DevBufOn gathered, gathered_lin, img, img_lin;  // on device 0
+  // the send slabs on every device, the gathered slabs and the image on device 0: the ctx's frame buffers,
+  // grown on demand (rt_ctx::FrameBuf), so that repeated frames allocate nothing
   int rc = RT_OK;
   for (int r = 0; r < n && !rc; ++r) {
     rt_ctx* d = dev_ctx(r);
-    if ((rc = send[r].alloc(d->device, (size_t)slab * 3))) break;
-    if (out_lin && (rc = send_lin[r].alloc(d->device, sizeof(double) * (size_t)slab * 3))) break;
+    DEVICE_SCOPE(d->device);
+    if ((rc = grow(d, d->fb_slab, (size_t)slab * 3))) break;
+    if (out_lin && (rc = grow(d, d->fb_slab_lin, sizeof(double) * (size_t)slab * 3))) break;
   }
-  if (!rc) rc = gathered.alloc(c->device, (size_t)n * slab * 3);
-  if (!rc && out_lin) rc = gathered_lin.alloc(c->device, sizeof(double) * (size_t)n * slab * 3);
-  if (!rc) rc = img.alloc(c->device, (size_t)npx * 3);
-  if (!rc && out_lin) rc = img_lin.alloc(c->device, sizeof(double) * (size_t)npx * 3);
+  {
+    DEVICE_SCOPE(c->device);
+    if (!rc) rc = grow(c, c->fb_gather, (size_t)n * slab * 3);
+    if (!rc && out_lin) rc = grow(c, c->fb_gather_lin, sizeof(double) * (size_t)n * slab * 3);
+    if (!rc) rc = grow(c, c->fb_img, (size_t)npx * 3);
+    if (!rc && out_lin) rc = grow(c, c->fb_img_lin, sizeof(double) * (size_t)npx * 3);
+  }
   if (rc) return rc;
+  void* gathered = c->fb_gather.p;
+  void* gathered_lin = c->fb_gather_lin.p;
+  void* img = c->fb_img.p;
+  void* img_lin = c->fb_img_lin.p;
   // the shards' renders, one per device, queued back to back
   for (int r = 0; r < n; ++r) {
     rt_ctx* d = dev_ctx(r);
     DEVICE_SCOPE(d->device);
     rt_render_params pr = p;
     pr.shard_rank = r;
-    if ((rc = launch_philox(d, cam, &pr, r, n, (uint8_t*)send[r].p, (double*)send_lin[r].p, d->stream))) return rc;
+    if ((rc = launch_philox(d, cam, &pr, r, n, (uint8_t*)d->fb_slab.p, out_lin ? (double*)d->fb_slab_lin.p : nullptr,
+                            d->stream)))
+      return rc;
     if (r == 0) HIPCHK(hipEventRecord(c->ev_gather, c->stream));
   }
   // the RCCL gather of the slabs to device 0 (rank 0), in the ranks' stream order after their renders
@@ -581,10 +608,10 @@ int render_multi(rt_ctx* c, const rt_camera* cam, rt_render_params p, uint8_t* o
     NCCLCHK(ncclGroupStart());
     for (int r = 0; r < n; ++r) {
       rt_ctx* d = dev_ctx(r);
-      const ncclResult_t g = ncclGather(send[r].p, r == 0 ? gathered.p : nullptr, (size_t)slab * 3, ncclUint8, 0,
+      const ncclResult_t g = ncclGather(d->fb_slab.p, r == 0 ? gathered : nullptr, (size_t)slab * 3, ncclUint8, 0,
                                         c->comms[r], d->stream);
       const ncclResult_t gl = g == ncclSuccess && out_lin
-                                  ? ncclGather(send_lin[r].p, r == 0 ? gathered_lin.p : nullptr, (size_t)slab * 3,
+                                  ? ncclGather(d->fb_slab_lin.p, r == 0 ? gathered_lin : nullptr, (size_t)slab * 3,
                                                ncclFloat64, 0, c->comms[r], d->stream)
                                   : g;
       if (gl != ncclSuccess) {
@@ -597,22 +624,22 @@ int render_multi(rt_ctx* c, const rt_camera* cam, rt_render_params p, uint8_t* o
   {
     DEVICE_SCOPE(c->device);
     HIPCHK(hipEventRecord(c->ev_gathered, c->stream));
-    if ((rc = rt_assemble_async(c, &p, (const uint8_t*)gathered.p, (uint8_t*)img.p, c->stream))) return rc;
-    if (out_lin &&
-        (rc = rt_assemble_linear_async(c, &p, (const double*)gathered_lin.p, (double*)img_lin.p, c->stream)))
+    if ((rc = rt_assemble_async(c, &p, (const uint8_t*)gathered, (uint8_t*)img, c->stream))) return rc;
+    if (out_lin && (rc = rt_assemble_linear_async(c, &p, (const double*)gathered_lin, (double*)img_lin, c->stream)))
       return rc;
     HIPCHK(hipEventRecord(c->ev_asm, c->stream));
   }
-  for (int r = 0; r < n; ++r) {  // (the peers' streams too: their slabs are freed on return)
+  for (int r = 0; r < n; ++r) {  // (the peers' streams too: the next frame reuses their slabs)
     rt_ctx* d = dev_ctx(r);
     DEVICE_SCOPE(d->device);
     HIPCHK(hipStreamSynchronize(d->stream));
   }
   DEVICE_SCOPE(c->device);
-  HIPCHK(hipMemcpy(out_rgb, img.p, (size_t)npx * 3, hipMemcpyDeviceToHost));
-  if (out_lin) HIPCHK(hipMemcpy(out_lin, img_lin.p, sizeof(double) * (size_t)npx * 3, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(out_rgb, img, (size_t)npx * 3, hipMemcpyDeviceToHost));
+  if (out_lin) HIPCHK(hipMemcpy(out_lin, img_lin, sizeof(double) * (size_t)npx * 3, hipMemcpyDeviceToHost));
   rt_frame_timing ft{};
   ft.n_devices = n;
+  for (int r = 0; r < n; ++r) ft.device_allocs += dev_ctx(r)->allocs;
   float ms = 0;
   for (int r = 0; r < n; ++r) {
     rt_ctx* d = dev_ctx(r);
@@ -740,6 +767,7 @@ void rt_destroy(rt_ctx* c) {
   c->peers.clear();
   DeviceGuard _dg(c->device);
   free_scene(c);
+  free_frame_bufs(c);
   (void)hipFree(c->d_counter);
   (void)hipFree(c->d_partial);
   (void)hipFree(c->d_tail);
@@ -918,27 +946,31 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, cons
       rt::set_error("rt_render: no scene uploaded on every device");
       return RT_E_STATE;
     }
+  c->allocs = 0;
+  for (rt_ctx* q : c->peers) q->allocs = 0;
   if (p.rng_mode == RT_RNG_PHILOX && !c->comms.empty()) return render_multi(c, cam, p, out_rgb, out_lin);
   DEVICE_SCOPE(c->device);
   const long long npx = (long long)p.width * p.height;
   hipStream_t st = c->stream;
-  DevBuf img, img_lin, slab_buf, slab_lin, gens;  // freed on every return path
-  HIPCHK(hipMalloc(&img.p, (size_t)npx * 3));
-  if (out_lin) HIPCHK(hipMalloc(&img_lin.p, sizeof(double) * (size_t)npx * 3));
-  uint8_t* d_img = (uint8_t*)img.p;
-  double* d_img_lin = (double*)img_lin.p;
+  // (the ctx's frame buffers, grown on demand: repeated frames allocate nothing)
+  if ((rc = grow(c, c->fb_img, (size_t)npx * 3))) return rc;
+  if (out_lin && (rc = grow(c, c->fb_img_lin, sizeof(double) * (size_t)npx * 3))) return rc;
+  uint8_t* d_img = (uint8_t*)c->fb_img.p;
+  double* d_img_lin = out_lin ? (double*)c->fb_img_lin.p : nullptr;
   rt_frame_timing ft{};
   ft.n_devices = 1;
   if (p.rng_mode == RT_RNG_PHILOX) {
     int tile, tiles_x;
     long long tt, ps, slab;
     geometry(&p, tile, tiles_x, tt, ps, slab);
-    HIPCHK(hipMalloc(&slab_buf.p, (size_t)slab * 3));
-    if (out_lin) HIPCHK(hipMalloc(&slab_lin.p, sizeof(double) * (size_t)slab * 3));
-    rc = launch_philox(c, cam, &p, 0, 1, (uint8_t*)slab_buf.p, (double*)slab_lin.p, st);
+    if ((rc = grow(c, c->fb_slab, (size_t)slab * 3))) return rc;
+    if (out_lin && (rc = grow(c, c->fb_slab_lin, sizeof(double) * (size_t)slab * 3))) return rc;
+    const uint8_t* slab_rgb = (const uint8_t*)c->fb_slab.p;
+    const double* slab_lin = out_lin ? (const double*)c->fb_slab_lin.p : nullptr;
+    rc = launch_philox(c, cam, &p, 0, 1, (uint8_t*)slab_rgb, (double*)slab_lin, st);
     if (!rc) rc = hip_ok(hipEventRecord(c->ev_gather, st), "hipEventRecord");
-    if (!rc) rc = rt_assemble_async(c, &p, (const uint8_t*)slab_buf.p, d_img, st);
-    if (!rc && out_lin) rc = rt_assemble_linear_async(c, &p, (const double*)slab_lin.p, d_img_lin, st);
+    if (!rc) rc = rt_assemble_async(c, &p, slab_rgb, d_img, st);
+    if (!rc && out_lin) rc = rt_assemble_linear_async(c, &p, slab_lin, d_img_lin, st);
     if (!rc) rc = hip_ok(hipEventRecord(c->ev_asm, st), "hipEventRecord");
     HIPCHK(hipStreamSynchronize(st));
     if (rc) return rc;
@@ -948,8 +980,8 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, cons
     ft.assemble_ms = a;
     ft.frame_ms = f;
   } else {
-    HIPCHK(hipMalloc(&gens.p, sizeof(uint64_t) * 2 * (size_t)p.width));
-    uint64_t* d_gens = (uint64_t*)gens.p;
+    if ((rc = grow(c, c->fb_gens, sizeof(uint64_t) * 2 * (size_t)p.width))) return rc;
+    uint64_t* d_gens = (uint64_t*)c->fb_gens.p;
     HIPCHK(hipMemcpyAsync(d_gens, col_gens, sizeof(uint64_t) * 2 * (size_t)p.width, hipMemcpyHostToDevice, st));
     RenderArgs A{};
     A.S = c->scene;
@@ -981,6 +1013,7 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* pin, cons
   c->last_ms = ms;
   ft.kernel_ms[0] = ms;
   if (p.rng_mode == RT_RNG_EXACT) ft.frame_ms = ms;
+  ft.device_allocs = c->allocs;
   c->last_frame = ft;
   return RT_OK;
 }

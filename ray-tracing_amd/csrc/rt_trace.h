@@ -925,13 +925,21 @@ template <unsigned F, class R>
 __device__ __forceinline__ void trav_media_first(const Scene& S, Trav& t, double t_min, Cnt& cnt, const R& g,
                                                  Side& side) {
   if constexpr ((F & F_MEDIA) != 0 && R::kKeyed) {
+    // A ray with a NaN in its origin or direction (the segment after a rect hit at t = NaN) hits nothing
+    // in the reference: its root box test fails (a NaN slab quotient, Lib.hs:798-814), so it never
+    // reaches a medium. The chain's box tests are skipped here, and a rect or cuboid boundary's t would be
+    // NaN, which the medium's range tests pass (a finite candidate): such a ray takes no candidate (ADVICE
+    // r5; the rest of the walk rejects it, set_ray32).
+    const bool dead = (t.ray.o.x != t.ray.o.x) | (t.ray.o.y != t.ray.o.y) | (t.ray.o.z != t.ray.o.z) |
+                      (t.ray.d.x != t.ray.d.x) | (t.ray.d.y != t.ray.d.y) | (t.ray.d.z != t.ray.d.z);
     for (;;) {
       if (!(t.node >= 0 && (t.node & (RT_WNODE | RT_IDTAGS)) == RT_ISBOX)) return;
       const rt_node* n = &S.nodes[t.node & ~(RT_SUB | RT_IDTAGS)];
       if (!(n->c & RT_BVH_MEDIA_FIRST)) return;
       const int m = n->a & ~RT_IDTAGS;
       if constexpr ((F & F_COUNT) != 0) ++cnt.other;
-      const double x = hoisted_medium_t<F>(S.nodes, m, t.ray, t_min, g.k0, g.k1, g.consumed(), g.sample, g.pid);
+      const double x =
+          dead ? -1.0 : hoisted_medium_t<F>(S.nodes, m, t.ray, t_min, g.k0, g.k1, g.consumed(), g.sample, g.pid);
       if (x >= 0.0 && x <= t.closest) trav_take<F>(S, t, x, m, kSubMedium, side, false, &S.nodes[m], false);
       t.node = n->b | RT_SUB;  // (the rest: below an ordered node, a re-bounded subtree)
     }
@@ -1134,17 +1142,38 @@ __device__ __forceinline__ bool wide_node(const Scene& S, Trav& t, int* stk, int
   return n_hit != 0;
 }
 
+// Trav::node values of a walk with a postponed leaf (Trav::pend): nothing left but that leaf (kNone); or
+// the next stack entry closes an instance frame, which must wait until the leaf — found inside that frame,
+// in its ray's coordinates — is tested (kHold, the mixed walk).
+constexpr int kNone = (int)0x80000000;
+constexpr int kHold = (int)0x80000001;
+
+// Leaf postponement in the mixed walk (media / frame worlds over 4-wide trees, F_MIXW; RT_MIXW_POSTPONE):
+// see walk_until.
+#ifndef RT_MIXW_POSTPONE
+#define RT_MIXW_POSTPONE 1
+#endif
+template <unsigned F>
+constexpr bool kMixPostpone = RT_MIXW_POSTPONE && (F & F_MIXW) != 0 && (F & F_WIDE) == 0;
+
 // Pop the next node of a binary (or mixed) walk; false once the walk is over. Frames that close
 // rebuild the parent's ray from the world ray, once for a run of them. (Mixed walks: leaf slots are
-// negative, so only a non-negative entry can be a frame marker.)
+// negative, so only a non-negative entry can be a frame marker.) `hold` (a postponed leaf is waiting,
+// kMixPostpone): a frame marker is not popped — the walk waits at it (kHold) — and an empty stack leaves
+// the walk on (kNone) for its leaf.
 template <unsigned F>
 __device__ __forceinline__ bool trav_pop_mixed(const Scene& S, Trav& t, const int* stk, int stride, Side& side,
-                                               double t_min = kEps) {
+                                               double t_min = kEps, bool hold = false) {
   bool reb = false;
   for (;;) {
     const bool end = t.sp == 0;
     const int e = end ? 0 : stk[(--t.sp) * stride];
     const bool frame = (F & F_FRAMES) && ((F & F_MIXW) ? (e >= 0 && (e & RT_FRAME)) : (e & RT_FRAME));
+    if (kMixPostpone<F> && hold && (end || frame)) {  // (reb is false: no frame closes while a leaf waits)
+      t.sp += end ? 0 : 1;
+      t.node = end ? kNone : kHold;
+      return true;
+    }
     if (end || !frame) {
       if ((F & F_FRAMES) && reb) {  // (also at the end: a tie redo walks on from it)
         // the parent's ray, once for the run of closed frames: the world ray rebuilt through the frames
@@ -1287,14 +1316,14 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
   } else {
     trav_leaf<F>(S, t, n, id, t_min, cnt, g, side, refsem);
   }
-  if (!to_wide) return trav_pop_mixed<F>(S, t, stk, stride, side, t_min);
+  if (!to_wide) return trav_pop_mixed<F>(S, t, stk, stride, side, t_min, t.pend >= 0);
   }
   if constexpr ((F & F_MIXW) != 0) {  // a 4-wide node (RT_WNODE | index)
     if constexpr ((F & F_COUNT) != 0) ++cnt.wide;
     refresh_ray32(t);
     if (wide_node<F>(S, t, stk, stride, t.node & ~RT_WNODE)) return true;
   }
-  return trav_pop_mixed<F>(S, t, stk, stride, side);
+  return trav_pop_mixed<F>(S, t, stk, stride, side, kEps, t.pend >= 0);
 }
 
 // ---- the 4-wide walk with postponed leaves (Aila & Laine's while-while, one postponed slot)
@@ -1303,7 +1332,6 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
 // searching for its first leaf. So wide-node steps and fp64 leaf tests do not share a divergent
 // step. Culling is looser while a leaf waits (its hit does not yet bound the walk); the closest
 // hit and the tie flag do not depend on the order leaves are tested in (trav_take).
-constexpr int kNone = (int)0x80000000;  // Trav::node: nothing left but the postponed leaf
 
 __device__ __forceinline__ int trav_pop(Trav& t, const int* stk, int stride) {
   return t.sp ? stk[(--t.sp) * stride] : kNone;
@@ -1342,6 +1370,66 @@ template <unsigned F, class R>
 __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walking, double t_min, int* stk, int stride,
                                            bool joint, int stop, int leaf_stop, Cnt& cnt, R& g, Side& side,
                                            int med_batch = 0) {
+  if constexpr (kMixPostpone<F>) {
+    // The mixed walk with postponed leaves (round 6; the 4-wide walk's scheme, Aila & Laine's while-while
+    // with one slot): a lane that reaches a leaf-table slot of a 4-wide tree (a primitive, a chain, or an
+    // instance frame to open) parks it in `pend` and walks on; the wave runs a leaf step — every lane holding
+    // a leaf tests it (or opens its frame) — once at most leaf_stop of its walking lanes can still step
+    // nodes. So wide / box steps and the leaf kinds' code do not share divergent steps (round 5's profile:
+    // steps mixing wide nodes with leaves and frames were 17 % of C4's steps and 53 % of its time). The
+    // closest hit is the least t over the leaves in any order (tier B: keyed media, re-bounded subtrees;
+    // exact ties are flagged and redone in the reference's order), culling is only looser while a leaf
+    // waits. A waiting leaf is tested in the coordinates it was found in: a lane holding one does not close
+    // an instance frame (kHold), and a parked frame opens in the leaf step above the lane's next node.
+    // Tie redos (t.redo) walk the caller's tree node by node, as before.
+    for (;;) {
+      if (__popcll(__ballot(walking)) <= stop) break;
+      const bool holding = walking && !t.redo && t.pend >= 0 && t.node < 0;  // (at a second leaf, kHold, kNone)
+      const bool seeking = walking && !holding;
+      unsigned kinds = 0;
+      unsigned long long t0 = 0;
+      const bool inner = __popcll(__ballot(seeking)) > leaf_stop || __ballot(holding) == 0;
+      if constexpr ((F & F_COUNT) != 0) {
+        ++(inner ? cnt.islot : cnt.lslot);
+        kinds = inner ? K_WIDE : K_LEAF;
+        t0 = stamp();
+      }
+      // inner step: the seeking lanes' nodes (a lane at a leaf slot only parks it, below); leaf step: the
+      // holding lanes' parked leaves — a leaf's test, or its frame opened — with the lane's next node (a
+      // second leaf slot) put back on the stack, unless the walk waits at a frame marker (kHold) or is done
+      // (kNone). One trav_step call site for both (a second inlined copy cost registers).
+      bool go;
+      if (inner) {
+        go = seeking && (t.redo || t.node >= 0);
+      } else {
+        go = holding;
+        if (holding) {
+          const int saved = t.node;
+          if (saved != kNone && saved != kHold) stk[(t.sp++) * stride] = saved;
+          t.node = ~t.pend;
+          t.pend = -1;
+        }
+      }
+      if (go) walking = trav_step<F>(S, t, t_min, stk, stride, joint, cnt, g, side) || t.pend >= 0;
+      // a leaf slot reached (by this step, or waiting since the last) with the slot free: park it, walk on
+      if (walking && !t.redo && t.pend < 0 && t.node < 0 && t.node != kNone && t.node != kHold) {
+        t.pend = ~t.node;
+        // (trav_pop_mixed with `hold`: the next entry, or wait at a frame marker, or nothing left)
+        const int e = t.sp ? stk[(t.sp - 1) * stride] : 0;
+        const bool fr = e >= 0 && (e & RT_FRAME);
+        t.node = t.sp == 0 ? kNone : (fr ? kHold : e);
+        t.sp -= (t.sp == 0 || fr) ? 0 : 1;
+      }
+      if constexpr ((F & F_COUNT) != 0) {
+        const unsigned long long t1 = stamp();
+        if (cnt.prof && __lane_id() == (unsigned)(__ffsll((long long)__ballot(true)) - 1)) {
+          atomicAdd(&cnt.prof[kinds], t1 - t0);
+          atomicAdd(&cnt.prof[32 + kinds], 1ull);
+        }
+      }
+    }
+    return;
+  }
   if constexpr ((F & F_WIDE) == 0) {
     for (;;) {
       const int n_walk = __popcll(__ballot(walking));

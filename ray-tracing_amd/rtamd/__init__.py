@@ -112,7 +112,7 @@ class rt_scene_info(C.Structure):
 
 
 class rt_frame_timing(C.Structure):
-    _fields_ = [("n_devices", C.c_int32), ("_pad", C.c_int32), ("kernel_ms", C.c_double * RT_MAX_DEVICES),
+    _fields_ = [("n_devices", C.c_int32), ("device_allocs", C.c_int32), ("kernel_ms", C.c_double * RT_MAX_DEVICES),
                 ("gather_ms", C.c_double), ("assemble_ms", C.c_double), ("frame_ms", C.c_double)]
 
 
@@ -535,10 +535,11 @@ class Context:
 
     def frame_timing(self) -> dict:
         """rt_last_frame_timing: per-device render kernel ms, RCCL gather ms, assemble ms, frame ms of the
-        last rt_render."""
+        last rt_render, and the device allocations it made (0 for a repeated frame of one size)."""
         t = rt_frame_timing()
         _check(lib().rt_last_frame_timing(self._h, C.byref(t)), "rt_last_frame_timing")
-        return {"n_devices": t.n_devices, "kernel_ms": [t.kernel_ms[i] for i in range(t.n_devices)],
+        return {"n_devices": t.n_devices, "device_allocs": t.device_allocs,
+                "kernel_ms": [t.kernel_ms[i] for i in range(t.n_devices)],
                 "gather_ms": t.gather_ms, "assemble_ms": t.assemble_ms, "frame_ms": t.frame_ms}
 
     def close(self):

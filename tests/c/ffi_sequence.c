@@ -10,12 +10,12 @@
  * way from its roots, then:
  *   CPU: checks the re-flattened descriptor is well formed for the library (rt_rebuild_bvh,
  *        rt_tree_stack_need) and that the duplication is what the Haskell module produces;
- *   GPU (argv[1] == "gpu"): runs runRenderAMD's sequence — rt_create_multi over every visible GPU
- *        (RenderAMD's default: the tile shards of a tier-B frame spread over the devices and gathered
- *        with RCCL), rt_upload_scene, rt_render in tier A with one (seed, gamma) per column (the
- *        deterministic app/Main.hs:47-49 harness: column 0 = the builder's g1, column x = randGen
- *        (1024 + x)) and in tier B, rt_destroy — and checks the bytes and end-of-stream generators equal
- *        those of the builder's own descriptor rendered on one device (rt_create). With argv[2] = a
+ *   GPU (argv[1] == "gpu"): runs runRenderAMD's sequence — rt_create(0), rt_upload_scene, rt_render in
+ *        tier A with one (seed, gamma) per column (the deterministic app/Main.hs:47-49 harness: column 0 =
+ *        the builder's g1, column x = randGen (1024 + x)), rt_destroy — and runRenderAMDPhilox's (the same
+ *        in tier B), and runRenderAMDPhiloxOn's (tier B on a rt_create_multi ctx over every visible GPU: the
+ *        tile shards spread over the devices and gathered with RCCL), and checks the bytes and end-of-stream
+ *        generators equal those of the builder's own descriptor rendered on one device. With argv[2] = a
  *        directory, it also writes <dir>/<scene>.bin: the flattened descriptor, the column generators
  *        and both tiers' outputs (RGB8, linear averages, tier-A end generators), which
  *        tests/test_ffi_sequence.py renders with the CPU oracle from the same flattened records.
@@ -221,29 +221,34 @@ static int run(int scene_id, const char* name, int cam_id, int W, int H, int spp
     gens[1] = g1[1];
     for (int x = 1; x < W; ++x) rt_rand_gen(1024 + x, gens + 2 * x);
     const size_t px = (size_t)W * H * 3;
-    uint8_t *rgb_a = malloc(px), *rgb_d[2] = {malloc(px), malloc(px)};
+    uint8_t *rgb_a = malloc(px), *rgb_d[2] = {malloc(px), malloc(px)}, *rgb_m = malloc(px);
     double* lin_d[2] = {malloc(px * 8), malloc(px * 8)};
     uint64_t *go_a = malloc(sizeof(uint64_t) * 2 * (size_t)W), *go_d = malloc(sizeof(uint64_t) * 2 * (size_t)W);
     for (int tier = 0; tier < 2 && !rc; ++tier) {
       rt_render_params p = {W, H, spp, 50, tier ? RT_RNG_PHILOX : RT_RNG_EXACT, 0, 1024, 16, 0, 1, 0};
-      for (int which = 0; which < 2 && !rc; ++which) {
-        /* runRenderAMD: rt_create_multi, rt_upload_scene, rt_render, rt_destroy (the builder's own
-           descriptor on one device: rt_create) */
+      /* which 0: the builder's own descriptor on one device; 1: runRenderAMD / runRenderAMDPhilox
+         (rt_create(0), rt_upload_scene of the flattened records, rt_render, rt_destroy); 2 (tier B):
+         runRenderAMDPhiloxOn over every visible GPU (rt_create_multi, tile shards gathered with RCCL) */
+      for (int which = 0; which < 2 + tier && !rc; ++which) {
         rt_ctx* ctx;
-        if (which ? rt_create_multi(ndev, NULL, &ctx) : rt_create(0, &ctx))
-          return fail(which ? "rt_create_multi" : "rt_create");
+        if (which == 2 ? rt_create_multi(ndev, NULL, &ctx) : rt_create(0, &ctx))
+          return fail(which == 2 ? "rt_create_multi" : "rt_create");
+        uint8_t* out = which == 0 ? rgb_a : (which == 1 ? rgb_d[tier] : rgb_m);
         if (rt_upload_scene(ctx, which ? &d : &a)) rc = fail("rt_upload_scene");
-        else if (rt_render(ctx, &cam, &p, gens, which ? rgb_d[tier] : rgb_a, which ? lin_d[tier] : NULL,
-                           which ? go_d : go_a))
+        else if (rt_render(ctx, &cam, &p, gens, out, which == 1 ? lin_d[tier] : NULL, which == 1 ? go_d : go_a))
           rc = fail("rt_render");
-        if (!rc && which && tier) {
+        if (!rc) {
           rt_frame_timing t;
-          if (rt_last_frame_timing(ctx, &t) || t.n_devices != ndev) rc = fail("rt_last_frame_timing");
+          if (rt_last_frame_timing(ctx, &t) || t.n_devices != (which == 2 ? ndev : 1)) rc = fail("rt_last_frame_timing");
         }
         rt_destroy(ctx);
       }
       if (!rc && memcmp(rgb_a, rgb_d[tier], px)) {
         fprintf(stderr, "FAIL %s: tier %c bytes differ\n", name, tier ? 'B' : 'A');
+        rc = 1;
+      }
+      if (!rc && tier && memcmp(rgb_a, rgb_m, px)) {
+        fprintf(stderr, "FAIL %s: tier B bytes differ on %d devices\n", name, ndev);
         rc = 1;
       }
       if (!rc && !tier && memcmp(go_a, go_d, sizeof(uint64_t) * 2 * (size_t)W)) {
@@ -256,7 +261,8 @@ static int run(int scene_id, const char* name, int cam_id, int W, int H, int spp
       fprintf(stderr, "FAIL %s: cannot write %s/%s.bin\n", name, dir, name);
       rc = 1;
     }
-    free(gens), free(rgb_a), free(rgb_d[0]), free(rgb_d[1]), free(lin_d[0]), free(lin_d[1]), free(go_a), free(go_d);
+    free(gens), free(rgb_a), free(rgb_d[0]), free(rgb_d[1]), free(rgb_m), free(lin_d[0]), free(lin_d[1]), free(go_a),
+        free(go_d);
   }
   if (!gpu && dir) { /* "dump" mode (no GPU): the flattened records and the generators, zero outputs */
     const size_t px = (size_t)W * H * 3;

@@ -45,9 +45,14 @@ def test_multi_device_ctx_equals_one_device_render(gpu_ctx, name, camname, w, h,
         try:
             assert m.devices() == devs
             m.upload(sc)
+            allocs = []
             for _ in range(2):  # (two frames over the same communicators)
                 rgb, lin, _ = m.render(cam, p, linear=True)
                 assert np.array_equal(rgb, ref) and np.array_equal(lin, lin_ref, equal_nan=True)
+                allocs.append(m.frame_timing()["device_allocs"])
+            # the ctx keeps its slabs, gathered slabs, image and chunk sums: a second frame of the same size
+            # allocates nothing on any device
+            assert allocs[0] > 0 and allocs[1] == 0, allocs
             t = m.frame_timing()
             print(f"{name} on devices {devs}: kernel {['%.3f' % k for k in t['kernel_ms']]} ms, RCCL gather "
                   f"{t['gather_ms']:.3f} ms, assemble {t['assemble_ms']:.3f} ms, frame {t['frame_ms']:.3f} ms")
@@ -57,6 +62,38 @@ def test_multi_device_ctx_equals_one_device_render(gpu_ctx, name, camname, w, h,
             assert np.array_equal(rgb_a, ref_a) and np.array_equal(gens_a, gens_ref)
         finally:
             m.close()
+
+
+def test_multi_device_ctx_full_c2_frame_costs_what_rt_render_costs(gpu_ctx):
+    """The bench frame (C2: book one 1200x800x500, depth 50) through a one-device rt_create_multi ctx
+    (slabs gathered by RCCL, assembled on device 0) against rt_render on a plain ctx: the same bytes, and
+    the blocking call's wall time within 1 % (min of 3 frames each, legs alternating), with no device
+    allocation after the first frame on either ctx."""
+    import time
+    sc, _ = rtamd.make_scene("random_book_one", rtamd.randGen(1024))
+    cam = rtamd.camera("random_scene", 1200, 800)
+    p = rtamd.make_params(1200, 800, 500, 50, rtamd.RT_RNG_PHILOX, seed=1024)
+    gpu_ctx.upload(sc)
+    m = rtamd.Context(devices=[0])
+    try:
+        m.upload(sc)
+        ref, _, _ = gpu_ctx.render(cam, p)  # (warm-up frames: kernels loaded, buffers grown)
+        got, _, _ = m.render(cam, p)
+        assert np.array_equal(got, ref)
+        wall = {"rt_render": [], "multi": []}
+        for _ in range(3):
+            for name, ctx in (("rt_render", gpu_ctx), ("multi", m)):
+                t0 = time.perf_counter()
+                ctx.render(cam, p)
+                wall[name].append(time.perf_counter() - t0)
+                assert ctx.frame_timing()["device_allocs"] == 0
+        a, b = min(wall["rt_render"]), min(wall["multi"])
+        t = m.frame_timing()
+        print(f"C2 frame: rt_render {a * 1e3:.2f} ms, rt_create_multi(1) {b * 1e3:.2f} ms ({(b / a - 1) * 100:+.2f} %); "
+              f"RCCL gather {t['gather_ms']:.3f} ms, assemble {t['assemble_ms']:.3f} ms")
+        assert b <= 1.01 * a
+    finally:
+        m.close()
 
 
 def test_multi_device_ctx_rejects_bad_lists():

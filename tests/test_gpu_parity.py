@@ -529,6 +529,49 @@ def test_nan_rays_hit_nothing(gpu_ctx, walk):
         assert per["prim_tests"] < 20 and per["wide_nodes"] < 60
 
 
+def test_nan_rays_take_no_hoisted_medium(gpu_ctx):
+    """the tier-B walk prelude takes a world's hoisted media (RT_BVH_MEDIA_FIRST) without the
+    chain's box tests. A ray with a NaN in its origin or direction (the segment after a rect hit at t = NaN)
+    fails the reference's root box test (src/Lib.hs:798-814) and so never reaches a medium; with a cuboid
+    boundary the boundary's t would be NaN, which the medium's range tests pass (a finite candidate). The
+    debug walk runs the render loop's prelude (rt_debug_closest_hits, RT_DEBUG_RESUMABLE): a fog with a
+    cuboid boundary over a 24-sphere world and a sky background, NaN rays and ordinary rays inside the fog,
+    against the oracle (the reference's recursion over the caller's tree)."""
+    b = rtamd.Builder(rtamd.randGen(7))
+    lam = b.lambertian(b.constantColor(0.7, 0.6, 0.5))
+    items = [b.sphere((3.0 * x, 1.0, 3.0 * z), 1.0, lam) for x in range(-3, 3) for z in range(-2, 2)]
+    fog = b.constantMedium(0.05, b.constantColor(1.0, 1.0, 1.0), b.cuboid((-20.0, -1.0, -20.0), (20.0, 10.0, 20.0), lam))
+    sc = b.finish(b.makeBVH((0.0, 1.0), items + [fog]), -1, (0.5, 0.7, 1.0))
+    rb = rtamd.rebuilt_scene(sc)
+    assert rb.nodes["c"][rb.desc.world_root] & rtamd.RT_BVH_MEDIA_FIRST  # (the fog is hoisted)
+    gpu_ctx.upload(sc)
+    rng = np.random.default_rng(11)
+    n = 1 << 14
+    o = rng.uniform(-15, 15, (n, 3))
+    o[:, 1] = rng.uniform(0, 8, n)
+    d = rng.normal(0, 1, (n, 3))
+    k = rng.integers(0, 6, n // 2)
+    o[np.arange(n // 2)[k < 3], k[k < 3]] = np.nan
+    d[np.arange(n // 2)[k >= 3], k[k >= 3] - 3] = np.nan
+    rays = np.concatenate([o, d, rng.uniform(0, 1, (n, 1))], axis=1)
+    got = gpu_ctx.closest_hits(rays, 1e-4, np.inf, seed=3, flags=rtamd.RT_DEBUG_RESUMABLE)
+    ref = pyoracle.closest_hits(sc, rays, 1e-4, np.inf, seed=3)
+    assert not ref[: n // 2, 0].any() and not got[: n // 2, 0].any(), "a NaN ray took a hit"
+    assert got[n // 2:, 0].sum() > n // 8
+    mats = sc.materials["type"]
+    same = np.all((got == ref) | (np.isnan(got) & np.isnan(ref)), axis=1)
+    med = (ref[:, 0] == 1) & (got[:, 11] == ref[:, 11]) & (mats[ref[:, 11].astype(int)] == 4)
+    close = med & (np.abs(got[:, 1] - ref[:, 1]) <= 8 * np.spacing(np.abs(ref[:, 1])))
+    print(f"hoisted cuboid fog: {int(med.sum())} medium hits, {int((~same).sum())} rays not bit-identical "
+          f"(medium t within 8 ulps: {bool(np.all(same | close))})")
+    bad = ~(same | close)
+    if bad.any():
+        import os
+        os.makedirs("gpurun_out", exist_ok=True)
+        np.savez("gpurun_out/hoisted_cuboid_fog.npz", rays=rays[bad], got=got[bad], ref=ref[bad])
+    assert not bad.any(), f"{int(bad.sum())} rays differ"
+
+
 def test_quantised_tree_renders_the_same_image(gpu_ctx, monkeypatch):
     """RTAMD_QNODE=1 (A/B: the global-memory spheres kernel over the quantised 64-byte nodes and the
     32-byte sphere leaves) renders the default build's image, bytes and linear averages."""

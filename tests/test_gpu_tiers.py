@@ -1,0 +1,80 @@
+"""Tier B against tier A as distributions, on the GPU.
+
+Tier B (RT_RNG_PHILOX) is the benchmarked path: one Philox stream per (pixel, sample), and since round 5
+its ConstantMedium draw is keyed by (walk, occurrence) with the candidate computed over the boundary's
+whole inside, then bounded (include/rt.h). Its GPU-vs-oracle tests compare it with the
+oracle's restatement of that same definition. Tier A (RT_RNG_EXACT) is the reference's own layout and
+semantics: one SplitMix generator per column threaded through every row, sample and bounce
+(src/Lib.hs:1491-1523), the medium's draw the stream's next under the walk's bound (src/Lib.hs:1053-1080),
+the time draw of getRay (src/Lib.hs:1253-1267) for moving spheres (src/Lib.hs:1106-1108); the GPU's tier A
+equals the oracle's bit for bit (test_gpu_parity.test_tier_a_rng_consuming_features). If tier B's draws are
+independent uniforms where the reference draws, both renders estimate the same image: here the same frame is
+rendered in both tiers and compared per 16x16 block and over the whole frame (tests/tier_stats.py):
+  * the finite part of the per-pixel average (RT_FLAG_NAN_ZERO on both sides), z of the block mean of the
+    pixel differences against its standard error;
+  * the NaN probability (the Lambertian light-mixture quirk, src/Lib.hs:829-835), on one-sample renders:
+    per-block two-proportion z.
+Scenes: cornell_smoke (media inside instance frames, real lights), next_week_final (keyed media hoisted
+out of the tree, the 1000-sphere instance frame, Perlin, the earth raster, motion blur), random (motion
+blur, checker), earth (image texture), simple_light (Perlin marble, real lights), two_perlin_spheres
+(NaN fraction: its lights are Unhittable and its background black, so every finite sample is 0).
+Under the null, the largest |z| of a scene's ~300-1000 block statistics is ~3-3.5; the bound is 5.5 per
+block and 4.5 for the whole frame's z (a false alarm below 1e-3 per scene)."""
+import os
+import time
+
+import numpy as np
+import pytest
+
+import rtamd
+from tier_stats import summary
+
+pytestmark = pytest.mark.gpu
+
+BLOCK = 16
+Z_BLOCK, Z_FRAME = 5.5, 4.5
+EARTH = os.path.join(os.path.dirname(__file__), "golden", "earthmap_rgb8.npz")
+
+# scene, camera, W, H, spp of the finite-part renders (the NaN renders: 1 spp), depth 50
+CASES = [
+    ("cornell_smoke", "cornell", 320, 320, 48),
+    ("next_week_final", "next_week", 320, 320, 16),
+    ("random", "random_scene", 480, 320, 24),
+    ("earth", "two_spheres", 480, 320, 24),
+    ("simple_light", "two_spheres", 480, 320, 32),
+    ("two_perlin_spheres", "two_spheres", 480, 320, 0),
+]
+
+
+@pytest.mark.parametrize("name,camname,W,H,spp", CASES)
+def test_tier_b_matches_tier_a_in_distribution(gpu_ctx, name, camname, W, H, spp):
+    earth = np.load(EARTH)["rgb"] if name in ("earth", "random", "next_week_final") else None
+    sc, g1 = rtamd.make_scene(name, rtamd.randGen(1024), earth=earth)
+    cam = rtamd.camera(camname, W, H)
+    gens = rtamd.column_gens(g1, W)
+    gpu_ctx.upload(sc)
+    t0 = time.perf_counter()
+    if spp:
+        pa = rtamd.make_params(W, H, spp, 50, rtamd.RT_RNG_EXACT, flags=rtamd.RT_FLAG_NAN_ZERO)
+        pb = rtamd.make_params(W, H, spp, 50, rtamd.RT_RNG_PHILOX, seed=1024, flags=rtamd.RT_FLAG_NAN_ZERO)
+        _, lin_a, _ = gpu_ctx.render(cam, pa, gens, linear=True)
+        t_a = time.perf_counter() - t0
+        _, lin_b, _ = gpu_ctx.render(cam, pb, linear=True)
+        assert np.isfinite(lin_a).all() and np.isfinite(lin_b).all()
+    else:
+        lin_a = lin_b = np.zeros((H, W, 3))
+        t_a = 0.0
+    # one sample per pixel: a pixel is NaN iff its sample is (the NaN probability, per block)
+    gens1 = rtamd.column_gens(g1, W, seed=50_000)  # (fresh column streams)
+    _, n_a, _ = gpu_ctx.render(cam, rtamd.make_params(W, H, 1, 50, rtamd.RT_RNG_EXACT), gens1, linear=True)
+    _, n_b, _ = gpu_ctx.render(cam, rtamd.make_params(W, H, 1, 50, rtamd.RT_RNG_PHILOX, seed=77), linear=True)
+    s = summary(lin_a, lin_b, np.isnan(n_a).any(axis=2), np.isnan(n_b).any(axis=2), BLOCK)
+    print(f"tiers {name} {W}x{H}x{spp} (+1 spp NaN renders), {s['blocks']} blocks of {BLOCK}x{BLOCK}: "
+          f"max |z| block mean {s['max_abs_z_block_mean']:.2f}, frame z {['%.2f' % z for z in s['z_frame_mean']]}; "
+          f"NaN fraction A {s['nan_frac'][0]:.4f} B {s['nan_frac'][1]:.4f}, max |z| block {s['max_abs_z_block_nan']:.2f}, "
+          f"frame z {s['z_frame_nan']:.2f}; frame mean A {['%.5f' % x for x in s['frame_mean'][0]]} "
+          f"B {['%.5f' % x for x in s['frame_mean'][1]]}; tier-A render {t_a:.1f} s")
+    if spp:
+        assert s["frame_mean"][0][0] > 0, "the finite part is empty: the comparison would be vacuous"
+    assert s["max_abs_z_block_mean"] <= Z_BLOCK and max(abs(z) for z in s["z_frame_mean"]) <= Z_FRAME
+    assert s["max_abs_z_block_nan"] <= Z_BLOCK and abs(s["z_frame_nan"]) <= Z_FRAME

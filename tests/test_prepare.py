@@ -166,6 +166,43 @@ def test_checker_children_must_precede_and_images_stay_in_pool():
         assert _code(_variant(e, textures=bad.view(e.textures.dtype))) == -1
 
 
+def test_medium_keys_all_or_none_and_distinct():
+    """tier-B medium draws are keyed per occurrence (include/rt.h; f[1] = key + 1 when the caller
+    sets it, else the occurrence's preorder rank). Caller keys are accepted only on every occurrence of the
+    world and only when distinct: a keyed record reached twice, or a caller key equal to an unkeyed
+    occurrence's rank, would make two occurrences draw the same numbers."""
+    s = _scene("next_week_final")
+    n0 = _nodes(s)
+    med = [int(i) for i in np.nonzero(n0["type"] == 9)[0]]
+    assert len(med) == 2
+    assert _code(s.desc) == 0
+
+    def with_keys(vals):
+        n = n0.copy()
+        for i, v in zip(med, vals):
+            n["f"][i, 1] = v
+        return _variant(s, nodes=n.view(s.nodes.dtype))
+
+    assert _code(with_keys([1.0, 2.0])) == 0      # every occurrence keyed, distinct
+    assert _code(with_keys([7.0, 3.0])) == 0
+    assert _code(with_keys([1.0, 0.0])) == -1     # keyed and unkeyed mixed (key 0 = the other's rank)
+    assert _code(with_keys([0.0, 5.0])) == -1
+    assert _code(with_keys([2.0, 2.0])) == -1     # one key twice
+    assert _code(with_keys([1.5, 2.0])) == -1     # not an integer
+    assert _code(with_keys([2.0 ** 32, 1.0])) == -1  # beyond the counter word's 31 bits
+    # BVHNode h h over a keyed medium (src/Lib.hs:948): one record reached along two paths
+    n = n0.copy()
+    n["f"][med[0], 1] = 1.0
+    n["f"][med[1], 1] = 2.0
+    parent = [i for i in _bvh_ids(n) if n["a"][i] == med[0] or n["b"][i] == med[0]][0]
+    n["a"][parent] = n["b"][parent] = med[0]
+    assert _code(_variant(s, nodes=n.view(s.nodes.dtype))) == -1
+    # the unfolded array (rt_rebuild_bvh: every occurrence keyed by its rank) prepares again as is
+    rb = rtamd.rebuilt_scene(s)
+    assert _code(rb.desc) == 0
+    assert (_nodes(rb)["f"][_nodes(rb)["type"] == 9][:, 1] >= 1).sum() >= 2
+
+
 def test_random_mutations_never_crash():
     """Seeded field mutations of valid descriptors: every call returns RT_OK or an error code (the
     sanitizer build runs the same loop natively, tests/c/host_check.cpp)."""
