@@ -238,8 +238,17 @@ bool flat_box(const std::vector<rt_node>& nodes, int id, Box* out) {
       if (!flat_box(nodes, n.a, &hb)) return false;
       const double s = n.f[0], c = n.f[1];
       double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+      // The reference's `rotate` bounds the rotated child over the points i, j, k in {0, 1, 2}
+      // (src/Lib.hs:732-761): the corners and points extrapolated a whole box extent beyond them, a box
+      // 3x as wide per axis. The re-bounded trees' boxes only cull (ties are redone on the caller's tree,
+      // which keeps the reference's boxes), so they bound the child by its 8 corners (rotation is
+      // linear), widened by 2^-30 of the magnitudes against rounding (round 6: the 1000-sphere frame of
+      // next_week_final was opened by every ray through its 27-times-larger box). RTAMD_TIGHT_ROTATE=0
+      // keeps the reference's box.
+      static const bool tight = !(std::getenv("RTAMD_TIGHT_ROTATE") && std::getenv("RTAMD_TIGHT_ROTATE")[0] == '0');
       for (int idx = 26; idx >= 0; --idx) {
         const double i = idx / 9, j = (idx / 3) % 3, k = idx % 3;
+        if (tight && (i > 1 || j > 1 || k > 1)) continue;
         const double p0 = i * hb.mx[0] + (1 - i) * hb.mn[0], p1 = j * hb.mx[1] + (1 - j) * hb.mn[1],
                      p2 = k * hb.mx[2] + (1 - k) * hb.mn[2];
         double q[3];
@@ -248,7 +257,11 @@ bool flat_box(const std::vector<rt_node>& nodes, int id, Box* out) {
         else { q[0] = c * p0 - s * p1; q[1] = s * p0 + c * p1; q[2] = p2; }
         for (int a = 0; a < 3; ++a) { mn[a] = gmin(q[a], mn[a]); mx[a] = gmax(q[a], mx[a]); }
       }
-      for (int a = 0; a < 3; ++a) { out->mn[a] = mn[a]; out->mx[a] = mx[a]; }
+      for (int a = 0; a < 3; ++a) {
+        const double pad = tight ? 0x1p-30 * (std::fabs(mn[a]) + std::fabs(mx[a]) + 1.0) : 0.0;
+        out->mn[a] = mn[a] - pad;
+        out->mx[a] = mx[a] + pad;
+      }
       return true;
     }
     case RT_NODE_CONSTANT_MEDIUM:

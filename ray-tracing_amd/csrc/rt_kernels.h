@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "rt.h"
@@ -382,9 +383,37 @@ __global__ void __launch_bounds__(WAVES * 256, WAVES) render_philox_lds(RenderAr
 // ended and starts their next segment (or sample, or pixel), then steps every walking lane one
 // node at a time until at most trav_stop/64 of the live lanes are still walking. Lanes never
 // wait for the slowest walk of their wave, and shading runs for many lanes at once.
+// The replacement loop's per-segment throughput and per-chunk sum: in registers, or (kStateLds: the compact
+// LDS-staged spheres kernel, RT_STATE_LDS) in the lane's LDS slots, so that they are not live across the
+// walk — the 4-wave kernel spilled them to scratch.
+#ifndef RT_STATE_LDS
+#define RT_STATE_LDS 1
+#endif
 template <unsigned F>
-__device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S, int* stk, int stride, int* side_p,
-                                             volatile uint32_t* wq) {
+constexpr bool kStateLds = RT_STATE_LDS && (F & F_SLEAF) != 0;
+template <bool LDS>
+struct LaneV3 {
+  V3 r;
+  double* p;
+  int stride;
+  __device__ __forceinline__ V3 get() const {
+    if constexpr (LDS) return v3(p[0], p[stride], p[2 * stride]);
+    return r;
+  }
+  __device__ __forceinline__ void set(V3 v) {
+    if constexpr (LDS) {
+      p[0] = v.x;
+      p[stride] = v.y;
+      p[2 * stride] = v.z;
+    } else {
+      r = v;
+    }
+  }
+};
+
+template <unsigned F, class STK>
+__device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S, STK* stk, int stride, int* side_p,
+                                             volatile uint32_t* wq, double* st = nullptr) {
   const int lane = threadIdx.x & 63;
   const unsigned long long lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const bool joint = !(A.flags & RT_FLAG_REFERENCE_CULL);
@@ -411,7 +440,8 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
   int& depth = kLaneLds ? ex[3 * stride] : l_depth;
   px = 0, row = 0, s_end = 0, depth = 0;
   int s = 0;
-  V3 thr = v3(0, 0, 0), sum = v3(0, 0, 0);
+  // (st: the lane's 6 LDS doubles, `stride` apart: throughput xyz, then the chunk's sum xyz)
+  LaneV3<kStateLds<F>> thr{v3(0, 0, 0), st, stride}, sum{v3(0, 0, 0), st + 3 * (kStateLds<F> ? stride : 0), stride};
   RngPhilox g;
   g.init(A.seed, 0, 0);
   Trav t;  // the segment's ray lives only here between segments (no second copy is carried)
@@ -427,16 +457,18 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
       ++samples;
     }
     if (A.flags & RT_FLAG_NAN_ZERO) contrib = nan_zero(contrib);
-    sum = sum + contrib;
+    const V3 sm = sum.get() + contrib;
+    sum.set(sm);
     ++s;
-    const bool all_nan = (A.flags & RT_FLAG_NAN_CULL) && sum.x != sum.x && sum.y != sum.y && sum.z != sum.z;
+    const bool all_nan = (A.flags & RT_FLAG_NAN_CULL) && sm.x != sm.x && sm.y != sm.y && sm.z != sm.z;
     if (s == s_end || all_nan) {
       // (a tail unit: its one sample's colour, summed in order with its chunk's others by tail_combine)
       if (kTail<F> && w >= kTailSlot) store_partial_at(A.tail_buf, w - kTailSlot, contrib);
-      else store_partial(A, w, sum);
+      else store_partial(A, w, sm);
       w = -1;
     }
   };
+  auto all_nan3 = [](V3 a) __attribute__((always_inline)) { return a.x != a.x && a.y != a.y && a.z != a.z; };
 
   for (;;) {
     unsigned long long s0 = 0;
@@ -450,7 +482,10 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
     // already: its colour is NaN whichever leaf the reference's order picks (NaN * anything, including
     // the background's 0, is NaN), and a tier-B sample's draws reach no other sample. (NaN-t hits come
     // from the Lambertian quirk's +x ray in a box top's plane, whose pdf is 0 / 0: DESIGN.md §4.3.)
-    if (ready && (t.tie || (kRefMixed<F> && t.lite)) && !t.redo && !(thr.x != thr.x && thr.y != thr.y && thr.z != thr.z)) {
+    // hoisted media, taken at the end of a first walk (RT_MEDIA_AFTER; rt_trace.h media_after)
+    if constexpr ((F & F_MEDIA) != 0)
+      if (ready && !t.redo) media_after<F>(S, t, kEps, cnt, g, side);
+    if (ready && (t.tie || (kRefMixed<F> && t.lite)) && !t.redo && !all_nan3(thr.get())) {
       ready = false;
       if constexpr ((F & F_COUNT) != 0) ++cnt.ties;
       trav_redo<F>(t, S.world_ref, INFINITY);
@@ -469,11 +504,13 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
       Ray ray = plain(t.ray);  // (every frame has closed: the world ray again)
       const bool got = trav_finish<F>(S, t, ray, kEps, h, side);
       V3 contrib;
-      if (shade_hit<F>(S, got, h, ray, thr, depth, g, contrib, cnt)) {
+      V3 th = thr.get();
+      if (shade_hit<F>(S, got, h, ray, th, depth, g, contrib, cnt)) {
         end_sample(contrib);
       } else if (depth <= 0) {  // rayColor's d <= 0 -> black (thr * 0 keeps a NaN throughput NaN)
-        end_sample(vmul(thr, v3(0.0, 0.0, 0.0)));
+        end_sample(vmul(th, v3(0.0, 0.0, 0.0)));
       } else {  // next segment of the same path
+        thr.set(th);
         t.ray.o = ray.o;
         t.ray.d = ray.d;
         t.ray.tm = ray.tm;
@@ -522,7 +559,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
             done = true;
           } else if (kTail<F> ? work_unit(A, (uint32_t)wi, px, row, s, s_end, w)
                               : work_item(A, (uint32_t)wi, px, row, s, s_end, w)) {
-            sum = v3(0, 0, 0);
+            sum.set(v3(0, 0, 0));
           } else {
             w = -1;
           }
@@ -546,10 +583,10 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
       t.ray.o = cray.o;
       t.ray.d = cray.d;
       t.ray.tm = cray.tm;
-      thr = v3(1.0, 1.0, 1.0);
+      thr.set(v3(1.0, 1.0, 1.0));
       depth = A.max_depth;
       if (depth <= 0) {
-        end_sample(vmul(thr, v3(0.0, 0.0, 0.0)));
+        end_sample(vmul(v3(1.0, 1.0, 1.0), v3(0.0, 0.0, 0.0)));
         continue;
       }
       start = true;
@@ -559,7 +596,8 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
       trav_begin<F>(t, plain(t.ray), S.world, kEps, INFINITY);
       // worlds with media or frames: the reference's order over the re-bounded skeleton
       if (S.ref_walk) trav_restart_ref(t, S.world, INFINITY);
-      trav_media_first<F>(S, t, kEps, cnt, g, side);  // (hoisted media: RT_BVH_MEDIA_FIRST)
+      trav_media_first<F>(S, t, kEps, cnt, g, side);  // (hoisted media: RT_BVH_MEDIA_FIRST, RT_MEDIA_AFTER=0)
+      t.node = media_rest<F>(S, t.node);               // (RT_MEDIA_AFTER: they are taken when the walk ends)
       walking = true;
     }
     if (!walking) break;  // this lane is finished; the rest of the wave carries on without it
@@ -630,6 +668,14 @@ __global__ void __launch_bounds__(WAVES * 256, WAVES)
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   __shared__ uint32_t wave_q[WAVES * 4][2];  // (static: kStaticLds bytes ahead of the dynamic LDS)
   constexpr int rec = (F & F_WIDE) ? (int)sizeof(rt_wnode) : (int)sizeof(rt_node);
+  // The compact form (F_SLEAF, round 6; spheres-only worlds): the leaf table staged as the leaves' 32-byte
+  // sphere quadruples (Scene::sleaves; the 64-byte records stay in global memory for trav_finish, once per
+  // segment), 16-bit lane stacks (the staged tree's node ids, leaf slots and — in tie redos — the flat ids
+  // of a world whose tree fits the LDS all fit 15 bits, and an F_WIDE kernel masks a flat id's kind tags off
+  // anyway), and the lanes' throughput and chunk sums in LDS (kStateLds): VERDICT r5 item 3.
+  constexpr bool kCompact = (F & F_SLEAF) != 0;
+  constexpr int lrec = kCompact ? 32 : (int)sizeof(rt_node);
+  using STK = typename std::conditional<kCompact, short, int>::type;
   {
     const uint4* src = (F & F_WIDE) ? reinterpret_cast<const uint4*>(A.S.wnodes)
                                     : reinterpret_cast<const uint4*>(A.S.nodes);
@@ -637,22 +683,31 @@ __global__ void __launch_bounds__(WAVES * 256, WAVES)
     const int n16 = n_nodes * (rec / 16);
     for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
     // F_WIDE: the leaf table too, when it fits (n_leaves > 0)
-    const uint4* lsrc = reinterpret_cast<const uint4*>(A.S.leaves);
+    const uint4* lsrc = kCompact ? reinterpret_cast<const uint4*>(A.S.sleaves) : reinterpret_cast<const uint4*>(A.S.leaves);
     uint4* ldst = reinterpret_cast<uint4*>(lds + (size_t)n_nodes * rec);
-    const int l16 = n_leaves * (int)(sizeof(rt_node) / 16);
+    const int l16 = n_leaves * (lrec / 16);
     for (int i = threadIdx.x; i < l16; i += blockDim.x) ldst[i] = lsrc[i];
   }
   __syncthreads();
   Scene S = A.S;
   if constexpr ((F & F_WIDE) != 0) S.wnodes = reinterpret_cast<const rt_wnode*>(lds);
   else S.nodes = reinterpret_cast<const rt_node*>(lds);
-  if constexpr (LEAF_LDS) S.leaves = reinterpret_cast<const rt_node*>(lds + (size_t)n_nodes * rec);
+  if constexpr (kCompact) S.sleaves = reinterpret_cast<const double*>(lds + (size_t)n_nodes * rec);
+  else if constexpr (LEAF_LDS) S.leaves = reinterpret_cast<const rt_node*>(lds + (size_t)n_nodes * rec);
   else n_leaves = 0;
-  int* stk = reinterpret_cast<int*>(lds + (size_t)n_nodes * rec + (size_t)n_leaves * sizeof(rt_node)) + threadIdx.x;
-  // (per lane: stack_entries stack ints, then side_ints_of Side slots, then lane_lds_of's 4 lane ints;
-  // launch_philox sizes the dynamic LDS with the same two helpers)
-  philox_loop2<F>(A, S, stk, WAVES * 256, stk + stack_entries * WAVES * 256,
-                  wave_q[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)]);
+  constexpr int lanes = WAVES * 256;
+  unsigned char* lane_base = lds + (size_t)n_nodes * rec + (size_t)n_leaves * lrec;
+  STK* stk = reinterpret_cast<STK*>(lane_base) + threadIdx.x;
+  // (per lane: stack_entries stack entries, then side_ints_of Side slots, then lane_lds_of's 4 lane ints —
+  // launch_philox sizes the dynamic LDS with the same helpers — and for kStateLds 6 doubles after them)
+  int* side_p = reinterpret_cast<int*>(lane_base + (size_t)stack_entries * lanes * sizeof(STK)) + threadIdx.x;
+  double* st = nullptr;
+  if constexpr (kStateLds<F>) {
+    const int side_total = side_ints_of(F, S.frames, 2) + (lane_lds_of(F, 2) ? 4 : 0);
+    st = reinterpret_cast<double*>(lane_base + (size_t)stack_entries * lanes * sizeof(STK) +
+                                   (size_t)side_total * lanes * sizeof(int)) + threadIdx.x;
+  }
+  philox_loop2<F>(A, S, stk, lanes, side_p, wave_q[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], st);
 }
 
 // The tail's work-items (work_unit): each chunk's sample colours added in sample order from 0, as the
@@ -805,9 +860,11 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
     Trav t;
     trav_begin<F>(t, r, S.world, tmin, tmax);
     if (S.ref_walk) trav_restart_ref(t, S.world, tmax);  // (the re-bounded skeleton, mixed walk)
-    trav_media_first<F>(S, t, tmin, cnt, g, side);        // (hoisted media: the render loop's walk prelude)
+    trav_media_first<F>(S, t, tmin, cnt, g, side);        // (hoisted media as the render loop takes them)
+    t.node = media_rest<F>(S, t.node);
     bool walking = true;
     walk_until<F>(S, t, walking, tmin, stk, RT_BLOCK, joint != 0, 0, 0, cnt, g, side);
+    media_after<F>(S, t, tmin, cnt, g, side);
     if (t.tie || (kRefMixed<F> && t.lite)) {
       trav_redo<F>(t, S.world_ref, tmax);
       while (trav_step<F>(S, t, tmin, stk, RT_BLOCK, joint != 0, cnt, g, side)) {
@@ -933,6 +990,12 @@ const void* pick_w(bool lds, int w, bool leaf_lds = false, bool q = false) {
       if (w == 3) return (const void*)render_philox2<V | F_QNODE, 3>;
       if (w == 4) return (const void*)render_philox2<V | F_QNODE, 4>;
       return (const void*)render_philox2<V | F_QNODE, 1>;
+    }
+  }
+  if constexpr (V == (kVarSpheres | F_WIDE)) {
+    if (lds && leaf_lds && q) {  // the compact LDS form: sphere quadruples, 16-bit stacks, state in LDS
+      if (w == 4) return (const void*)render_philox2_lds<V | F_SLEAF, 4, true>;
+      if (w == 3) return (const void*)render_philox2_lds<V | F_SLEAF, 3, true>;
     }
   }
   if constexpr ((V & F_WIDE) != 0) {

@@ -64,8 +64,10 @@ enum : unsigned {
                   // re-bounded subtrees (RT_WROOT nodes) instead of walking them node by node
   F_SLIBM = 2048u, // tier A with RT_FLAG_SHARED_LIBM: sin / cos / log / atan / asin from include/rt_libm.h
                    // (the oracle's too) instead of OCML
-  F_QNODE = 4096u  // (spheres-only F_WIDE kernels reading the tree from global memory) the quantised 4-wide
+  F_QNODE = 4096u, // (spheres-only F_WIDE kernels reading the tree from global memory) the quantised 4-wide
                    // nodes (rt_qnode) and the leaves' sphere quadruples instead of the 128 / 64-byte records
+  F_SLEAF = 8192u  // (spheres-only F_WIDE kernels) leaf tests read the leaves' 32-byte sphere quadruples
+                   // (Scene::sleaves, staged in LDS by the compact kernel) instead of the 64-byte records
 };
 
 // Kernel variants: spheres-only (configs 1, 2, 5), Cornell-like (rects, instances, lights), full.

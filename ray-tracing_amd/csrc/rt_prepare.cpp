@@ -452,20 +452,20 @@ int prepare_scene(const rt_scene_desc* din, uint32_t flags, PreparedScene& P) {
           }
           w.child[k] = ~slot[id];
         }
-      // spheres-only worlds, RTAMD_QNODE=1 (A/B only): the compact forms (rt_qnode, sphere quadruples)
-      // beside the full records, for the global-memory kernels. Measured on C5 at 100 spp, same box:
+      // spheres-only worlds: the leaves' 32-byte sphere quadruples (centre, radius) beside the full
+      // records — the compact LDS-staged kernel stages them (round 6) — and, RTAMD_QNODE=1 (A/B only), the
+      // quantised nodes (rt_qnode) for the global-memory kernels. Measured on C5 at 100 spp, same box:
       // 1023 ms with 128-byte nodes, 1173 with quantised nodes (the plane decoding's VALU), 1030 with
       // only the 32-byte sphere leaves: the walk is not bound by the tree's footprint
-      const char* qenv = std::getenv("RTAMD_QNODE");
-      bool spheres = variant_for(P.features) == kVarSpheres && qenv && qenv[0] == '1';
+      bool spheres = variant_for(P.features) == kVarSpheres;
       for (const rt_node& x : leaves) spheres &= (x.type & RT_TYPE_MASK) == RT_NODE_SPHERE;
-      if (spheres && quantize_wide(wide, P.qnodes)) {
+      if (spheres) {
         P.sleaves.resize(4 * leaves.size());
         for (size_t i = 0; i < leaves.size(); ++i)
           for (int k = 0; k < 4; ++k) P.sleaves[4 * i + k] = leaves[i].f[k];
-      } else {
-        P.qnodes.clear();
       }
+      const char* qenv = std::getenv("RTAMD_QNODE");
+      if (!(spheres && qenv && qenv[0] == '1' && quantize_wide(wide, P.qnodes))) P.qnodes.clear();
       P.wnodes = std::move(wide);
       P.leaves = std::move(leaves);
       P.wide_stack_need = std::max(need, v.stack_need[unfolded]);

@@ -513,9 +513,21 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
     const int items = wide ? c->n_wnodes : c->n_nodes;
     const size_t rec = wide ? sizeof(rt_wnode) : sizeof(rt_node);
     const bool leaf_lds = wide && !env_off("RTAMD_LEAF_LDS");  // RTAMD_LEAF_LDS=0: leaves never in LDS
+    // The compact form of a spheres-only world's 4-wide kernel (F_SLEAF, rt_kernels.h render_philox2_lds):
+    // 32-byte sphere leaves, 16-bit lane stacks (ids below 2^15), the lanes' throughput and chunk sums in
+    // LDS; RTAMD_COMPACT=0: the 64-byte leaf records and 32-bit stacks
+    const bool compact = var == kVarSpheres && wide && leaf_lds && waves >= 3 && c->d_sleaves && c->n_nodes < 32768 &&
+                         c->n_wnodes < 32768 && c->n_leaves <= 32768 && !env_off("RTAMD_COMPACT");
+    constexpr size_t kStateBytes = kStateLds<kVarSpheres | F_WIDE | F_SLEAF> ? 6 * sizeof(double) : 0;
     // LDS bytes at `w` waves per SIMD: the nodes, the lane stacks, and the wide walk's leaf table
     // when it fits as well
     auto lds_bytes = [&](int w, int& n_leaves) {
+      if (compact) {
+        const size_t b = (size_t)items * rec + ((size_t)entries * sizeof(short) + (size_t)side_ints * sizeof(int) +
+                                                kStateBytes) * (w * 256);
+        n_leaves = c->n_leaves;
+        return b + (size_t)n_leaves * 32;
+      }
       size_t b = (size_t)items * rec + (size_t)(entries + side_ints) * (w * 256) * sizeof(int);
       n_leaves = leaf_lds && b + (size_t)c->n_leaves * sizeof(rt_node) <= kLdsBudget ? c->n_leaves : 0;
       return b + (size_t)n_leaves * sizeof(rt_node);
@@ -528,7 +540,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
     const int block = waves * 256;
     const size_t bytes = lds_bytes(waves, n_leaves);
     if (bytes <= kLdsBudget) {
-      const void* fn = philox_kernel(var, loop, true, waves, false, n_leaves > 0);
+      const void* fn = philox_kernel(var, loop, true, waves, false, n_leaves > 0, compact);
       HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
       int n_items = items;
       void* args[] = {&A, &n_items, (void*)&entries, &n_leaves};
@@ -802,7 +814,7 @@ int upload_prepared(rt_ctx* c, const rt::PreparedScene& P, const rt_scene_desc* 
       (rc = upload(&c->d_wnodes, P.wnodes.data(), P.wnodes.size())) ||
       (rc = upload(&c->d_leaves, P.leaves.data(), P.leaves.size())) ||
       (rc = upload(&c->d_qnodes, P.qnodes.data(), P.qnodes.size())) ||
-      (rc = upload(&c->d_sleaves, P.sleaves.data(), P.qnodes.empty() ? 0 : P.sleaves.size()))) {
+      (rc = upload(&c->d_sleaves, P.sleaves.data(), P.sleaves.size()))) {
     free_scene(c);
     return rc;
   }

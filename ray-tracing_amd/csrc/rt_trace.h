@@ -323,6 +323,20 @@ __device__ __forceinline__ bool prim_t(const Scene& S, const rt_node* n, const R
     return sphere_t(sc, e->f[3], r, t_min, t_max, t);
   }
   if constexpr (!(F & F_RECT)) return false;
+#if RT_CUBOID_TIMING_PROBE
+  // (timing probe only, wrong hits: a plain slab test in place of the six faces — the bound on what a
+  // cheaper exact cuboid test could save)
+  if (type == RT_NODE_CUBOID) {
+    double L = t_min, U = t_max;
+    for (int a = 0; a < 3; ++a) {
+      const double ta = (n->f[a] - comp(r.o, a)) * comp(r.inv, a), tb = (n->f[a + 3] - comp(r.o, a)) * comp(r.inv, a);
+      L = fmax(L, fmin(ta, tb));
+      U = fmin(U, fmax(ta, tb));
+    }
+    t = L;
+    return L <= U && L > t_min;
+  }
+#endif
   if (type == RT_NODE_CUBOID) {
     bool have = false;
     for (int i = 5; i >= 0; --i) {
@@ -891,11 +905,14 @@ __device__ __forceinline__ void trav_take(const Scene& S, Trav& t, double x, int
 }
 // A hoisted medium's tier-B candidate (RT_BVH_MEDIA_FIRST, rt_bvh.cpp): exactly the walk's medium leaf
 // (trav_leaf: boundary queries over (-inf, inf) and (t1 + eps, inf), the keyed draw, OCML's log), or -1
-// when the ray draws no hit in it (a candidate is >= t_min > 0). Not inlined: it runs where lanes start
-// their walks, and inlined it would be a second copy of the primitive tests in the render loop.
+// when the ray draws no hit in it (a candidate is >= t_min > 0), or — `bound`, the walk's closest hit when
+// the media are taken after it (RT_MEDIA_AFTER) — when the candidate is certainly beyond `bound`, which
+// trav_take would not take anyway. That is decided without the fp64 log where an fp32 lower bound of the
+// drawn distance already exceeds the room left (below); otherwise the exact expression decides.
 template <unsigned F>
 __device__ __forceinline__ double hoisted_medium_t(const rt_node* nodes, int id, RayX rx, double t_min, uint32_t k0,
-                                                uint32_t k1, uint32_t walk, uint32_t sample, uint32_t pid) {
+                                                uint32_t k1, uint32_t walk, uint32_t sample, uint32_t pid,
+                                                double bound = INFINITY) {
   Scene S{};
   S.nodes = nodes;
   const rt_node* n = &nodes[id];
@@ -913,17 +930,54 @@ __device__ __forceinline__ double hoisted_medium_t(const rt_node* nodes, int id,
   const double ray_length = vlen(rx.d);
   const double dist_inside = (t2 - rec1t) * ray_length;
   const double rnd = RngPhilox::keyed_at(k0, k1, walk, sample, pid, medium_key(n));
+  // The log skipped where it cannot matter (round 6): hit_dist = |f0| * (-log rnd), f0 = -1/density. With
+  // r32 >= rnd (fp32, rounded up) -log(r32) <= -log(rnd), and OCML's logf is within 2 ulp (2^-22 relative), so
+  // lo = |f0| * (-logf(r32)) * (1 - 2^-20) <= hit_dist. The candidate is used only when hit_dist <= dist_inside
+  // and rec1t + hit_dist / ray_length <= bound; lo beyond both (the second with a relative slack of 2^-30 and
+  // an absolute one of 2^-40 (|rec1t| + |bound|) ray_length, for the roundings of the quotient and the sum)
+  // rejects it exactly as the fp64 expression would. A thin fog's mean free path is far beyond most walks'
+  // closest hits (next_week_final's whole-scene fog: 10 000 units against hits ~100 away), so most draws end
+  // here.
+  {
+    float r32 = (float)rnd;
+    r32 = (double)r32 < rnd ? __int_as_float(__float_as_int(r32) + 1) : r32;
+    const double lo = fabs(n->f[0]) * (double)(-logf(r32)) * (1.0 - 0x1p-20);
+    const double room = fmin(dist_inside, (bound - rec1t) * ray_length * (1.0 + 0x1p-30) +
+                                              0x1p-40 * (fabs(rec1t) + fabs(bound)) * ray_length);
+    if (lo > room) return -1.0;
+  }
   const double hit_dist = n->f[0] * log_call(rnd);  // (not inlined: log_call)
   if (hit_dist > dist_inside) return -1.0;
   return rec1t + (hit_dist / ray_length);
 }
-// The walk's prelude (tier B, worlds with hoisted media): the RT_BVH_MEDIA_FIRST chain at the top of the
-// world is taken here, each medium's candidate offered to trav_take like a leaf of a re-bounded subtree,
-// without the chain's box tests (they only cull; the medium tests are exact), so that the walk starts at
-// the rest of the world already bounded by the media. Lanes run it where they start walks together.
+// RT_MEDIA_AFTER (round 6, the default): a world's hoisted media are taken when the walk over the rest of the
+// world has ended (media_after, at the closest hit the walk found) instead of where it starts (the prelude,
+// trav_media_first): the candidate is the same number (the keyed draw names the walk by the stream words
+// consumed, which no walk changes), the closest hit is the least t either way and a medium candidate at exactly
+// a surface's t is flagged as a tie either way (trav_take), but at the end the bound is known, so most draws
+// skip the fp64 log (hoisted_medium_t). The walk then starts below the chain (media_rest).
+#ifndef RT_MEDIA_AFTER
+#define RT_MEDIA_AFTER 1
+#endif
+template <unsigned F>
+__device__ __forceinline__ int media_rest(const Scene& S, int node) {
+  if constexpr ((F & F_MEDIA) != 0 && RT_MEDIA_AFTER) {
+    for (;;) {
+      if (!(node >= 0 && (node & (RT_WNODE | RT_IDTAGS)) == RT_ISBOX)) return node;
+      const rt_node* n = &S.nodes[node & ~(RT_SUB | RT_IDTAGS)];
+      if (!(n->c & RT_BVH_MEDIA_FIRST)) return node;
+      node = n->b | RT_SUB;  // (the rest: below an ordered node, a re-bounded subtree)
+    }
+  }
+  return node;
+}
+// The hoisted media chain from `node` (S.world): each medium's candidate offered to trav_take like a leaf of a
+// re-bounded subtree, without the chain's box tests (they only cull; the medium tests are exact). `after`:
+// the walk over the rest has ended (t.closest is its closest hit, t.node is not touched); else the prelude,
+// which leaves t.node at the rest.
 template <unsigned F, class R>
-__device__ __forceinline__ void trav_media_first(const Scene& S, Trav& t, double t_min, Cnt& cnt, const R& g,
-                                                 Side& side) {
+__device__ __forceinline__ void media_chain(const Scene& S, Trav& t, double t_min, Cnt& cnt, const R& g, Side& side,
+                                            int node, bool after) {
   if constexpr ((F & F_MEDIA) != 0 && R::kKeyed) {
     // A ray with a NaN in its origin or direction (the segment after a rect hit at t = NaN) hits nothing
     // in the reference: its root box test fails (a NaN slab quotient, Lib.hs:798-814), so it never
@@ -933,17 +987,34 @@ __device__ __forceinline__ void trav_media_first(const Scene& S, Trav& t, double
     const bool dead = (t.ray.o.x != t.ray.o.x) | (t.ray.o.y != t.ray.o.y) | (t.ray.o.z != t.ray.o.z) |
                       (t.ray.d.x != t.ray.d.x) | (t.ray.d.y != t.ray.d.y) | (t.ray.d.z != t.ray.d.z);
     for (;;) {
-      if (!(t.node >= 0 && (t.node & (RT_WNODE | RT_IDTAGS)) == RT_ISBOX)) return;
-      const rt_node* n = &S.nodes[t.node & ~(RT_SUB | RT_IDTAGS)];
-      if (!(n->c & RT_BVH_MEDIA_FIRST)) return;
+      if (!(node >= 0 && (node & (RT_WNODE | RT_IDTAGS)) == RT_ISBOX)) break;
+      const rt_node* n = &S.nodes[node & ~(RT_SUB | RT_IDTAGS)];
+      if (!(n->c & RT_BVH_MEDIA_FIRST)) break;
       const int m = n->a & ~RT_IDTAGS;
       if constexpr ((F & F_COUNT) != 0) ++cnt.other;
-      const double x =
-          dead ? -1.0 : hoisted_medium_t<F>(S.nodes, m, t.ray, t_min, g.k0, g.k1, g.consumed(), g.sample, g.pid);
+      // (a NaN closest hit — a rect hit at t = NaN, flagged for a redo — takes no medium: x <= NaN is false)
+      const double x = dead ? -1.0
+                            : hoisted_medium_t<F>(S.nodes, m, t.ray, t_min, g.k0, g.k1, g.consumed(), g.sample, g.pid,
+                                                  after ? t.closest : INFINITY);
       if (x >= 0.0 && x <= t.closest) trav_take<F>(S, t, x, m, kSubMedium, side, false, &S.nodes[m], false);
-      t.node = n->b | RT_SUB;  // (the rest: below an ordered node, a re-bounded subtree)
+      node = n->b | RT_SUB;
     }
+    if (!after) t.node = node;
   }
+}
+// The walk's prelude (RT_MEDIA_AFTER=0; tier B, worlds with hoisted media): the chain at the top of the world
+// taken where lanes start their walks together, so that the walk starts at the rest already bounded by the
+// media.
+template <unsigned F, class R>
+__device__ __forceinline__ void trav_media_first(const Scene& S, Trav& t, double t_min, Cnt& cnt, const R& g,
+                                                 Side& side) {
+  if constexpr (!RT_MEDIA_AFTER) media_chain<F>(S, t, t_min, cnt, g, side, t.node, false);
+}
+// RT_MEDIA_AFTER: the chain taken at the end of a first walk (not a tie redo, which walks the caller's tree,
+// media included), before the tie check.
+template <unsigned F, class R>
+__device__ __forceinline__ void media_after(const Scene& S, Trav& t, double t_min, Cnt& cnt, const R& g, Side& side) {
+  if constexpr (RT_MEDIA_AFTER) media_chain<F>(S, t, t_min, cnt, g, side, S.world, true);
 }
 // A leaf: a primitive, an instance chain ending in one (its t and face only: the record is built once,
 // in trav_finish), or a ConstantMedium (ref walks only: its one draw happens here, in the reference's
@@ -955,7 +1026,7 @@ __device__ __forceinline__ void trav_media_first(const Scene& S, Trav& t, double
 template <unsigned F, class R>
 __device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, const rt_node* n, int id, double t_min, Cnt& cnt,
                                           R& g, Side& side, bool refsem) {
-  if constexpr ((F & F_QNODE) != 0) {
+  if constexpr ((F & (F_QNODE | F_SLEAF)) != 0) {
     if (id & kSlotTag) {  // a leaf-table slot of a spheres-only world: its (center, radius) quadruple
       if constexpr ((F & F_COUNT) != 0) ++cnt.prim;
       const double2* q = reinterpret_cast<const double2*>(S.sleaves + 4 * (size_t)(id & ~kSlotTag));
@@ -1087,8 +1158,8 @@ __device__ __forceinline__ float4 qplanes(uint32_t q, float s, float o) {
 // One wide node (index `w`): test the four child boxes, enter the nearest accepted child, stack the
 // others (farthest deepest). F_QNODE: the node is read in its quantised form (64 bytes) and its planes
 // decoded; the test over them is the same.
-template <unsigned F = 0>
-__device__ __forceinline__ bool wide_node(const Scene& S, Trav& t, int* stk, int stride, int w) {
+template <unsigned F = 0, class STK>
+__device__ __forceinline__ bool wide_node(const Scene& S, Trav& t, STK* stk, int stride, int w) {
   float4 nx, ny, nz, fx, fy, fz;
   int4 ch;
   if constexpr ((F & F_QNODE) != 0) {
@@ -1148,10 +1219,11 @@ __device__ __forceinline__ bool wide_node(const Scene& S, Trav& t, int* stk, int
 constexpr int kNone = (int)0x80000000;
 constexpr int kHold = (int)0x80000001;
 
-// Leaf postponement in the mixed walk (media / frame worlds over 4-wide trees, F_MIXW; RT_MIXW_POSTPONE):
-// see walk_until.
+// Leaf postponement in the mixed walk (media / frame worlds over 4-wide trees, F_MIXW; RT_MIXW_POSTPONE=1,
+// A/B only): see walk_until. Measured slower (C4 at 100 spp, same box: 150.5 / 152.7 ms without, 164.4 /
+// 166.1 with; leaf-step thresholds 1 / 8 / 16 of 64: 170-174 / 166 / 188 ms), so off by default.
 #ifndef RT_MIXW_POSTPONE
-#define RT_MIXW_POSTPONE 1
+#define RT_MIXW_POSTPONE 0
 #endif
 template <unsigned F>
 constexpr bool kMixPostpone = RT_MIXW_POSTPONE && (F & F_MIXW) != 0 && (F & F_WIDE) == 0;
@@ -1161,8 +1233,8 @@ constexpr bool kMixPostpone = RT_MIXW_POSTPONE && (F & F_MIXW) != 0 && (F & F_WI
 // negative, so only a non-negative entry can be a frame marker.) `hold` (a postponed leaf is waiting,
 // kMixPostpone): a frame marker is not popped — the walk waits at it (kHold) — and an empty stack leaves
 // the walk on (kNone) for its leaf.
-template <unsigned F>
-__device__ __forceinline__ bool trav_pop_mixed(const Scene& S, Trav& t, const int* stk, int stride, Side& side,
+template <unsigned F, class STK>
+__device__ __forceinline__ bool trav_pop_mixed(const Scene& S, Trav& t, const STK* stk, int stride, Side& side,
                                                double t_min = kEps, bool hold = false) {
   bool reb = false;
   for (;;) {
@@ -1196,8 +1268,8 @@ __device__ __forceinline__ bool trav_pop_mixed(const Scene& S, Trav& t, const in
 // (Translate/Rotate over a BVH, Lib.hs:1029-1052): a tagged stack entry, the frame's id in the
 // lane's Side slots, and the child's ray in Trav::ray; when the entry is popped the parent's ray is
 // rebuilt from the world ray through the frames still open (the same operations as on entry).
-template <unsigned F, class R>
-__device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min, int* stk, int stride, bool joint,
+template <unsigned F, class R, class STK>
+__device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min, STK* stk, int stride, bool joint,
                                           Cnt& cnt, R& g, Side& side) {
   bool wide = false;
   if constexpr ((F & F_WIDE) != 0) wide = !t.ref;
@@ -1333,24 +1405,26 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
 // step. Culling is looser while a leaf waits (its hit does not yet bound the walk); the closest
 // hit and the tie flag do not depend on the order leaves are tested in (trav_take).
 
-__device__ __forceinline__ int trav_pop(Trav& t, const int* stk, int stride) {
+template <class STK>
+__device__ __forceinline__ int trav_pop(Trav& t, const STK* stk, int stride) {
   return t.sp ? stk[(--t.sp) * stride] : kNone;
 }
 // node -> pend when node is a leaf and the slot is free, then continue with the next stack entry
-__device__ __forceinline__ void trav_postpone(Trav& t, const int* stk, int stride) {
+template <class STK>
+__device__ __forceinline__ void trav_postpone(Trav& t, const STK* stk, int stride) {
   if (t.node < 0 && t.node != kNone && t.pend < 0) {
     t.pend = ~t.node;
     t.node = trav_pop(t, stk, stride);
   }
 }
-template <unsigned F>
-__device__ __forceinline__ void wide_inner(const Scene& S, Trav& t, int* stk, int stride, Cnt& cnt) {
+template <unsigned F, class STK>
+__device__ __forceinline__ void wide_inner(const Scene& S, Trav& t, STK* stk, int stride, Cnt& cnt) {
   if constexpr ((F & F_COUNT) != 0) ++cnt.wide;
   if (!wide_node<F>(S, t, stk, stride, t.node)) t.node = trav_pop(t, stk, stride);
   trav_postpone(t, stk, stride);
 }
-template <unsigned F, class R>
-__device__ __forceinline__ void wide_leaf(const Scene& S, Trav& t, double t_min, int* stk, int stride, Cnt& cnt, R& g,
+template <unsigned F, class R, class STK>
+__device__ __forceinline__ void wide_leaf(const Scene& S, Trav& t, double t_min, STK* stk, int stride, Cnt& cnt, R& g,
                                           Side& side) {
   if (t.pend >= 0) {
     const rt_node* n = &S.leaves[t.pend];  // (pend holds the leaf table slot)
@@ -1366,8 +1440,8 @@ __device__ __forceinline__ void wide_leaf(const Scene& S, Trav& t, double t_min,
 // wait), so that one step runs the box test alone instead of every node kind its lanes are at
 // (leaf_stop >= the live lanes: every step runs every lane). 4-wide walks: wide-node steps until at
 // most `leaf_stop` walking lanes still look for their first leaf, then one leaf step.
-template <unsigned F, class R>
-__device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walking, double t_min, int* stk, int stride,
+template <unsigned F, class R, class STK>
+__device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walking, double t_min, STK* stk, int stride,
                                            bool joint, int stop, int leaf_stop, Cnt& cnt, R& g, Side& side,
                                            int med_batch = 0) {
   if constexpr (kMixPostpone<F>) {

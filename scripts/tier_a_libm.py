@@ -122,6 +122,16 @@ def main():
                             **{f"{n}_s": t[f"oracle_{n}_s"] for n in ("glibc", "rt_libm")})
     lines = [compare("oracle glibc vs oracle rt_libm.h (CPU proxy)", res["glibc"], res["rt_libm"], a.spp, full)]
     if a.gpu:
+        # (a full-frame tier-A launch runs for minutes — one lane per column, every row and sample in
+        # series: print a heartbeat so that the run is seen to be alive)
+        import threading
+        stop = threading.Event()
+
+        def beat():
+            t_start = time.time()
+            while not stop.wait(30):
+                print(f"  ... tier-A GPU render running, {time.time() - t_start:.0f} s", flush=True)
+        threading.Thread(target=beat, daemon=True).start()
         ctx = rtamd.Context(0)
         ctx.upload(sc)
         for name, flags in (("ocml", 0), ("gpu_rt_libm", rtamd.RT_FLAG_SHARED_LIBM)):
@@ -131,6 +141,7 @@ def main():
             t[f"gpu_{name}_s"] = time.time() - t0
             res[name] = (rgb, lin, go)
         ctx.close()
+        stop.set()
         lines.append(compare("GPU OCML (runRenderAMD) vs oracle glibc", res["ocml"], res["glibc"], a.spp, full))
         same = compare("GPU rt_libm.h vs oracle rt_libm.h", res["gpu_rt_libm"], res["rt_libm"], a.spp)
         lines.append(same)

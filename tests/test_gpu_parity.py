@@ -148,7 +148,10 @@ def test_tier_a_rng_consuming_features(gpu_ctx, name, camname, w, h, spp):
     print(f"  columns with equal end generators: channels within 1e-3 {ok_c:.6f}, bytes equal {eq_c:.6f}; oracle "
           f"glibc vs rt_libm.h: channels within 1e-3 {ok_l:.6f}, end generators equal in "
           f"{(gens_s == gens_o).all(axis=1).mean():.6f} of columns")
-    assert same_cols.mean() >= 0.5 and ok_c >= 0.999 and eq_c >= 0.999
+    # measured (rounds 5-6, deterministic on a given device libm): 47 of 48 columns keep the glibc draw count at
+    # 48x48x3; the bound allows one more column to diverge (~2.5e-5 divergences per sample on
+    # this scene, none on Cornell or book one at their full bench frames)
+    assert same_cols.mean() >= 0.95 and ok_c >= 0.999 and eq_c >= 0.999
     assert (gens_s == gens_o).all(axis=1).mean() < 1.0  # (the libm swap alone diverges columns too)
 
 
@@ -559,7 +562,11 @@ def test_nan_rays_take_no_hoisted_medium(gpu_ctx):
     assert not ref[: n // 2, 0].any() and not got[: n // 2, 0].any(), "a NaN ray took a hit"
     assert got[n // 2:, 0].sum() > n // 8
     mats = sc.materials["type"]
-    same = np.all((got == ref) | (np.isnan(got) & np.isnan(ref)), axis=1)
+    # (sphere u, v go through atan / asin: OCML vs glibc, within 2e-15; every other field exact, or for a
+    # medium hit its t through log within 8 ulps)
+    ex = [0, 1, 2, 3, 4, 5, 6, 7, 10, 11]
+    same = np.all((got[:, ex] == ref[:, ex]) | (np.isnan(got[:, ex]) & np.isnan(ref[:, ex])), axis=1)
+    same &= np.all(np.abs(got[:, 8:10] - ref[:, 8:10]) <= 2e-15, axis=1)
     med = (ref[:, 0] == 1) & (got[:, 11] == ref[:, 11]) & (mats[ref[:, 11].astype(int)] == 4)
     close = med & (np.abs(got[:, 1] - ref[:, 1]) <= 8 * np.spacing(np.abs(ref[:, 1])))
     print(f"hoisted cuboid fog: {int(med.sum())} medium hits, {int((~same).sum())} rays not bit-identical "
