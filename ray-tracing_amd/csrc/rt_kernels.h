@@ -386,11 +386,23 @@ __global__ void __launch_bounds__(WAVES * 256, WAVES) render_philox_lds(RenderAr
 // The replacement loop's per-segment throughput and per-chunk sum: in registers, or (kStateLds: the compact
 // LDS-staged spheres kernel, RT_STATE_LDS) in the lane's LDS slots, so that they are not live across the
 // walk — the 4-wave kernel spilled them to scratch.
+// RT_STATE_LDS: 1 throughput and sum, 2 the throughput only, 0 neither. The compact form's parts are
+// separable for A/B runs: RT_COMPACT_STACK16 (16-bit stacks), RT_COMPACT_SLEAF (32-byte sphere leaves).
 #ifndef RT_STATE_LDS
 #define RT_STATE_LDS 1
 #endif
+#ifndef RT_COMPACT_STACK16
+#define RT_COMPACT_STACK16 1
+#endif
+#ifndef RT_COMPACT_SLEAF
+#define RT_COMPACT_SLEAF 1
+#endif
 template <unsigned F>
-constexpr bool kStateLds = RT_STATE_LDS && (F & F_SLEAF) != 0;
+constexpr bool kStateLds = RT_STATE_LDS != 0 && (F & F_SLEAF) != 0;
+template <unsigned F>
+constexpr bool kSumLds = RT_STATE_LDS == 1 && (F & F_SLEAF) != 0;
+// LDS bytes per lane the compact form keeps its state in
+constexpr int kStateLdsBytes = RT_STATE_LDS == 1 ? 48 : (RT_STATE_LDS == 2 ? 24 : 0);
 template <bool LDS>
 struct LaneV3 {
   V3 r;
@@ -441,7 +453,8 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
   px = 0, row = 0, s_end = 0, depth = 0;
   int s = 0;
   // (st: the lane's 6 LDS doubles, `stride` apart: throughput xyz, then the chunk's sum xyz)
-  LaneV3<kStateLds<F>> thr{v3(0, 0, 0), st, stride}, sum{v3(0, 0, 0), st + 3 * (kStateLds<F> ? stride : 0), stride};
+  LaneV3<kStateLds<F>> thr{v3(0, 0, 0), st, stride};
+  LaneV3<kSumLds<F>> sum{v3(0, 0, 0), st + 3 * (kSumLds<F> ? stride : 0), stride};
   RngPhilox g;
   g.init(A.seed, 0, 0);
   Trav t;  // the segment's ray lives only here between segments (no second copy is carried)
@@ -674,8 +687,9 @@ __global__ void __launch_bounds__(WAVES * 256, WAVES)
   // of a world whose tree fits the LDS all fit 15 bits, and an F_WIDE kernel masks a flat id's kind tags off
   // anyway), and the lanes' throughput and chunk sums in LDS (kStateLds): VERDICT r5 item 3.
   constexpr bool kCompact = (F & F_SLEAF) != 0;
-  constexpr int lrec = kCompact ? 32 : (int)sizeof(rt_node);
-  using STK = typename std::conditional<kCompact, short, int>::type;
+  constexpr bool kSleaf = kCompact && RT_COMPACT_SLEAF;
+  constexpr int lrec = kSleaf ? 32 : (int)sizeof(rt_node);
+  using STK = typename std::conditional<kCompact && RT_COMPACT_STACK16, short, int>::type;
   {
     const uint4* src = (F & F_WIDE) ? reinterpret_cast<const uint4*>(A.S.wnodes)
                                     : reinterpret_cast<const uint4*>(A.S.nodes);
@@ -683,7 +697,7 @@ __global__ void __launch_bounds__(WAVES * 256, WAVES)
     const int n16 = n_nodes * (rec / 16);
     for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
     // F_WIDE: the leaf table too, when it fits (n_leaves > 0)
-    const uint4* lsrc = kCompact ? reinterpret_cast<const uint4*>(A.S.sleaves) : reinterpret_cast<const uint4*>(A.S.leaves);
+    const uint4* lsrc = kSleaf ? reinterpret_cast<const uint4*>(A.S.sleaves) : reinterpret_cast<const uint4*>(A.S.leaves);
     uint4* ldst = reinterpret_cast<uint4*>(lds + (size_t)n_nodes * rec);
     const int l16 = n_leaves * (lrec / 16);
     for (int i = threadIdx.x; i < l16; i += blockDim.x) ldst[i] = lsrc[i];
@@ -692,7 +706,7 @@ __global__ void __launch_bounds__(WAVES * 256, WAVES)
   Scene S = A.S;
   if constexpr ((F & F_WIDE) != 0) S.wnodes = reinterpret_cast<const rt_wnode*>(lds);
   else S.nodes = reinterpret_cast<const rt_node*>(lds);
-  if constexpr (kCompact) S.sleaves = reinterpret_cast<const double*>(lds + (size_t)n_nodes * rec);
+  if constexpr (kSleaf) S.sleaves = reinterpret_cast<const double*>(lds + (size_t)n_nodes * rec);
   else if constexpr (LEAF_LDS) S.leaves = reinterpret_cast<const rt_node*>(lds + (size_t)n_nodes * rec);
   else n_leaves = 0;
   constexpr int lanes = WAVES * 256;

@@ -515,18 +515,21 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
     const bool leaf_lds = wide && !env_off("RTAMD_LEAF_LDS");  // RTAMD_LEAF_LDS=0: leaves never in LDS
     // The compact form of a spheres-only world's 4-wide kernel (F_SLEAF, rt_kernels.h render_philox2_lds):
     // 32-byte sphere leaves, 16-bit lane stacks (ids below 2^15), the lanes' throughput and chunk sums in
-    // LDS; RTAMD_COMPACT=0: the 64-byte leaf records and 32-bit stacks
+    // LDS. Opt-in (RTAMD_COMPACT=1): measured slower on C2
+    const char* ce = std::getenv("RTAMD_COMPACT");
     const bool compact = var == kVarSpheres && wide && leaf_lds && waves >= 3 && c->d_sleaves && c->n_nodes < 32768 &&
-                         c->n_wnodes < 32768 && c->n_leaves <= 32768 && !env_off("RTAMD_COMPACT");
-    constexpr size_t kStateBytes = kStateLds<kVarSpheres | F_WIDE | F_SLEAF> ? 6 * sizeof(double) : 0;
+                         c->n_wnodes < 32768 && c->n_leaves <= 32768 && ce && ce[0] == '1';
+    constexpr size_t kStateBytes = kStateLdsBytes;
+    constexpr size_t kStackBytes = RT_COMPACT_STACK16 ? sizeof(short) : sizeof(int);
+    constexpr size_t kLeafBytes = RT_COMPACT_SLEAF ? 32 : sizeof(rt_node);
     // LDS bytes at `w` waves per SIMD: the nodes, the lane stacks, and the wide walk's leaf table
     // when it fits as well
     auto lds_bytes = [&](int w, int& n_leaves) {
       if (compact) {
-        const size_t b = (size_t)items * rec + ((size_t)entries * sizeof(short) + (size_t)side_ints * sizeof(int) +
+        const size_t b = (size_t)items * rec + ((size_t)entries * kStackBytes + (size_t)side_ints * sizeof(int) +
                                                 kStateBytes) * (w * 256);
         n_leaves = c->n_leaves;
-        return b + (size_t)n_leaves * 32;
+        return b + (size_t)n_leaves * kLeafBytes;
       }
       size_t b = (size_t)items * rec + (size_t)(entries + side_ints) * (w * 256) * sizeof(int);
       n_leaves = leaf_lds && b + (size_t)c->n_leaves * sizeof(rt_node) <= kLdsBudget ? c->n_leaves : 0;

@@ -307,6 +307,35 @@ __device__ __forceinline__ void cuboid_face(const rt_node* n, int i, int& plane,
   k = (i & 1) ? (plane == 0 ? z0 : (plane == 1 ? y0 : x0)) : (plane == 0 ? z1 : (plane == 1 ? y1 : x1));
 }
 
+// A cuboid the ray certainly misses within [t_min, t_max] (round 6): the joint slab interval of its box,
+// division-free as box_hit computes it, empty by a margin of 2^-40 of the magnitudes involved (the
+// quotients' and the faces' in-plane coordinates' roundings are ~2^-52 of them). Then no face can pass
+// rectHit (Lib.hs:1014-1028): at a face's t the ray lies in that face's plane, so another axis's slab must
+// exclude it, by more than the face test's rounding of that coordinate. Zero direction components give
+// +-inf products, exact (outside a slab it is parallel to: L = +inf or U = -inf, and that face pair's t are
+// +-inf, out of range); a NaN product (the origin on such a slab's plane), a NaN bound or a ray box_hit
+// cannot bound (ray_safe) decides nothing: the six faces decide. Rays that start on a box they are leaving
+// (a bounce off a box top) reach its leaf under the 4-wide test's slack and are the common case here.
+#ifndef RT_CUBOID_PRETEST
+#define RT_CUBOID_PRETEST 1
+#endif
+__device__ __forceinline__ bool cuboid_missed(const double* f, const RayX& r, double t_min, double t_max) {
+  double L = t_min, U = t_max, K = 0.0;
+  bool nan = (t_min != t_min) | (t_max != t_max);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const double o = comp(r.o, a), y = comp(r.inv, a);
+    const double ta = (f[a] - o) * y, tb = (f[a + 3] - o) * y;
+    nan |= (ta != ta) | (tb != tb);
+    L = fmax(L, fmin(ta, tb));
+    U = fmin(U, fmax(ta, tb));
+    K = fmax(K, isinf(y) ? 0.0 : fabs(o * y));
+  }
+  const double band = 0x1p-40 * (fabs(L) + fabs(U) + K);
+  const bool ok_band = (band > 0x1p-1000) & (band < INFINITY);
+  return ray_safe(r) & !nan & ((ok_band & (L - U > band)) | (L == INFINITY) | (U == -INFINITY));
+}
+
 // Leaf primitives (Sphere, MovingSphere, Rect{XY,XZ,YZ}, Cuboid): the t of a hit and, for a
 // cuboid, which face (`sub`) won. hit Cuboid (Lib.hs:989-1004) is foldr closerHit over the six
 // faces, each with the full [tmin, tmax]: the later face keeps a tie.
@@ -338,6 +367,7 @@ __device__ __forceinline__ bool prim_t(const Scene& S, const rt_node* n, const R
   }
 #endif
   if (type == RT_NODE_CUBOID) {
+    if (RT_CUBOID_PRETEST && cuboid_missed(n->f, r, t_min, t_max)) return false;
     bool have = false;
     for (int i = 5; i >= 0; --i) {
       int plane;
@@ -909,6 +939,9 @@ __device__ __forceinline__ void trav_take(const Scene& S, Trav& t, double x, int
 // the media are taken after it (RT_MEDIA_AFTER) — when the candidate is certainly beyond `bound`, which
 // trav_take would not take anyway. That is decided without the fp64 log where an fp32 lower bound of the
 // drawn distance already exceeds the room left (below); otherwise the exact expression decides.
+#ifndef RT_LOG_PREFILTER
+#define RT_LOG_PREFILTER 1
+#endif
 template <unsigned F>
 __device__ __forceinline__ double hoisted_medium_t(const rt_node* nodes, int id, RayX rx, double t_min, uint32_t k0,
                                                 uint32_t k1, uint32_t walk, uint32_t sample, uint32_t pid,
@@ -938,7 +971,7 @@ __device__ __forceinline__ double hoisted_medium_t(const rt_node* nodes, int id,
   // rejects it exactly as the fp64 expression would. A thin fog's mean free path is far beyond most walks'
   // closest hits (next_week_final's whole-scene fog: 10 000 units against hits ~100 away), so most draws end
   // here.
-  {
+  if (RT_LOG_PREFILTER) {
     float r32 = (float)rnd;
     r32 = (double)r32 < rnd ? __int_as_float(__float_as_int(r32) + 1) : r32;
     const double lo = fabs(n->f[0]) * (double)(-logf(r32)) * (1.0 - 0x1p-20);
@@ -950,14 +983,16 @@ __device__ __forceinline__ double hoisted_medium_t(const rt_node* nodes, int id,
   if (hit_dist > dist_inside) return -1.0;
   return rec1t + (hit_dist / ray_length);
 }
-// RT_MEDIA_AFTER (round 6, the default): a world's hoisted media are taken when the walk over the rest of the
+// RT_MEDIA_AFTER (round 6, A/B only: measured slower, C4 at 100 spp 158.4 vs 145.4-147.6 ms — without the
+// media's bound the walks visit 10 % more nodes, 33.2 vs 30.1 wide nodes per sample): a world's hoisted
+// media are taken when the walk over the rest of the
 // world has ended (media_after, at the closest hit the walk found) instead of where it starts (the prelude,
 // trav_media_first): the candidate is the same number (the keyed draw names the walk by the stream words
 // consumed, which no walk changes), the closest hit is the least t either way and a medium candidate at exactly
 // a surface's t is flagged as a tie either way (trav_take), but at the end the bound is known, so most draws
 // skip the fp64 log (hoisted_medium_t). The walk then starts below the chain (media_rest).
 #ifndef RT_MEDIA_AFTER
-#define RT_MEDIA_AFTER 1
+#define RT_MEDIA_AFTER 0
 #endif
 template <unsigned F>
 __device__ __forceinline__ int media_rest(const Scene& S, int node) {
@@ -1026,7 +1061,10 @@ __device__ __forceinline__ void media_after(const Scene& S, Trav& t, double t_mi
 template <unsigned F, class R>
 __device__ __forceinline__ void trav_leaf(const Scene& S, Trav& t, const rt_node* n, int id, double t_min, Cnt& cnt,
                                           R& g, Side& side, bool refsem) {
-  if constexpr ((F & (F_QNODE | F_SLEAF)) != 0) {
+#ifndef RT_COMPACT_SLEAF
+#define RT_COMPACT_SLEAF 1
+#endif
+  if constexpr ((F & F_QNODE) != 0 || ((F & F_SLEAF) != 0 && RT_COMPACT_SLEAF)) {
     if (id & kSlotTag) {  // a leaf-table slot of a spheres-only world: its (center, radius) quadruple
       if constexpr ((F & F_COUNT) != 0) ++cnt.prim;
       const double2* q = reinterpret_cast<const double2*>(S.sleaves + 4 * (size_t)(id & ~kSlotTag));
