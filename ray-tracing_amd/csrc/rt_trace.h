@@ -316,8 +316,10 @@ __device__ __forceinline__ void cuboid_face(const rt_node* n, int i, int& plane,
 // +-inf, out of range); a NaN product (the origin on such a slab's plane), a NaN bound or a ray box_hit
 // cannot bound (ray_safe) decides nothing: the six faces decide. Rays that start on a box they are leaving
 // (a bounce off a box top) reach its leaf under the 4-wide test's slack and are the common case here.
+// Measured (round 6, A/B only): inlined into the walk it raised the C4 kernel's scratch 176 -> 288 B/lane and
+// C4 at 100 spp 146.9 -> 166.0 ms (C3 98.6 -> 99.9); out of line, 304 B/lane. Off.
 #ifndef RT_CUBOID_PRETEST
-#define RT_CUBOID_PRETEST 1
+#define RT_CUBOID_PRETEST 0
 #endif
 __device__ __forceinline__ bool cuboid_missed(const double* f, const RayX& r, double t_min, double t_max) {
   double L = t_min, U = t_max, K = 0.0;
@@ -369,6 +371,11 @@ __device__ __forceinline__ bool prim_t(const Scene& S, const rt_node* n, const R
   if (type == RT_NODE_CUBOID) {
     if (RT_CUBOID_PRETEST && cuboid_missed(n->f, r, t_min, t_max)) return false;
     bool have = false;
+#if RT_CUBOID_UNROLL == 1
+#pragma unroll
+#elif RT_CUBOID_UNROLL == 2
+#pragma nounroll
+#endif
     for (int i = 5; i >= 0; --i) {
       int plane;
       double a0, a1, b0, b1, k, tt;
@@ -939,8 +946,9 @@ __device__ __forceinline__ void trav_take(const Scene& S, Trav& t, double x, int
 // the media are taken after it (RT_MEDIA_AFTER) — when the candidate is certainly beyond `bound`, which
 // trav_take would not take anyway. That is decided without the fp64 log where an fp32 lower bound of the
 // drawn distance already exceeds the room left (below); otherwise the exact expression decides.
+// (measured neutral with the media taken in the prelude, C4 at 100 spp 165.1-166.9 vs 165.4-166.4 ms: off)
 #ifndef RT_LOG_PREFILTER
-#define RT_LOG_PREFILTER 1
+#define RT_LOG_PREFILTER 0
 #endif
 template <unsigned F>
 __device__ __forceinline__ double hoisted_medium_t(const rt_node* nodes, int id, RayX rx, double t_min, uint32_t k0,
