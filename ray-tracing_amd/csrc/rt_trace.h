@@ -1632,8 +1632,14 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
       const bool seeking = walking && (t.ref || (t.pend < 0 && t.node >= 0));
       const bool holding = walking && !t.ref && t.pend >= 0;
       // (every walking lane is seeking or holding, so one of the two steps always makes progress)
+      unsigned kinds = 0;
+      unsigned long long t0 = 0;
+      if constexpr ((F & F_COUNT) != 0) t0 = stamp();
       if (__popcll(__ballot(seeking)) > leaf_stop || __ballot(holding) == 0) {
-        if constexpr ((F & F_COUNT) != 0) ++cnt.islot;
+        if constexpr ((F & F_COUNT) != 0) {
+          ++cnt.islot;
+          kinds = __ballot(walking && t.ref) ? K_BOX | K_WIDE : K_WIDE;
+        }
         if (walking && t.ref) {
           walking = trav_step<F>(S, t, t_min, stk, stride, joint, cnt, g, side);
         } else if (walking && t.node >= 0) {
@@ -1641,10 +1647,20 @@ __device__ __forceinline__ void walk_until(const Scene& S, Trav& t, bool& walkin
           walking = t.node != kNone || t.pend >= 0;
         }
       } else {
-        if constexpr ((F & F_COUNT) != 0) ++cnt.lslot;
+        if constexpr ((F & F_COUNT) != 0) {
+          ++cnt.lslot;
+          kinds = K_LEAF;
+        }
         if (holding) {
           wide_leaf<F>(S, t, t_min, stk, stride, cnt, g, side);
           walking = t.node != kNone || t.pend >= 0;
+        }
+      }
+      if constexpr ((F & F_COUNT) != 0) {  // (step profile: wide steps, tie-redo steps, leaf steps)
+        const unsigned long long t1 = stamp();
+        if (cnt.prof && __lane_id() == (unsigned)(__ffsll((long long)__ballot(true)) - 1)) {
+          atomicAdd(&cnt.prof[kinds], t1 - t0);
+          atomicAdd(&cnt.prof[32 + kinds], 1ull);
         }
       }
     }
