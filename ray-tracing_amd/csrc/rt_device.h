@@ -81,6 +81,18 @@ constexpr bool kSL = (F & F_SLIBM) != 0;
 // a - b*q is exact under FMA when nothing under- or overflows), then a range guard that falls back
 // to the IEEE division unless |a|, |b| and |q| all lie in [2^-900, 2^900] (zero, tiny, huge and
 // non-finite operands included). Bit-identical to `a / b` (tests/test_gpu_math.py).
+// The IEEE division of the rare operands. RT_DIV_CALL=1 puts it out of line, one copy per kernel instead of
+// one per inlined quotient (the C4 kernel inlines 157 IEEE divisions, ~1.9 k of its 14.1 k instructions, and
+// its 83.5 KB of code miss the instruction cache: 102 M misses per launch, profiles/r6_pmc_c4.json); the call
+// raised its scratch 176 -> 192 B/lane (round 6), so it stays inline.
+#ifndef RT_DIV_CALL
+#define RT_DIV_CALL 0
+#endif
+#if RT_DIV_CALL
+__device__ __noinline__ double ieee_div(double a, double b) { return a / b; }
+#else
+__device__ __forceinline__ double ieee_div(double a, double b) { return a / b; }
+#endif
 __device__ __forceinline__ bool in_range(double x) {
   const double ax = fabs(x);
   return (ax >= 0x1p-900) & (ax <= 0x1p900);
@@ -91,7 +103,7 @@ __device__ __forceinline__ double div_exact(double a, double b, double y) {
   q = fma(r, y, q);
   r = fma(-q, b, a);
   q = fma(r, y, q);
-  if (!(in_range(a) && in_range(b) && in_range(q))) q = a / b;
+  if (!(in_range(a) && in_range(b) && in_range(q))) q = ieee_div(a, b);
   return q;
 }
 
@@ -134,7 +146,7 @@ __device__ __forceinline__ double qdiv(double a, double d, double y) {
   q = fma(r, y, q);
   const bool zero = d == 0.0;
   q = zero ? a * y : q;
-  if (!(zero | (in_range(a) & in_range(d) & in_range(q)))) q = a / d;
+  if (!(zero | (in_range(a) & in_range(d) & in_range(q)))) q = ieee_div(a, d);
   return q;
 }
 struct Hit {

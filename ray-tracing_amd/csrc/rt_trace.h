@@ -217,8 +217,8 @@ __device__ __forceinline__ bool sphere_t(V3 sc, double sr, const RayX& r, double
   const double n1 = (-b) - sd, n2 = (-b) + sd;
   double temp1 = div_mk(n1, a, inva), temp2 = div_mk(n2, a, inva);
   if (!(in_range(a) & q_ok(n1, temp1) & q_ok(n2, temp2))) {
-    temp1 = n1 / a;
-    temp2 = n2 / a;
+    temp1 = ieee_div(n1, a);
+    temp2 = ieee_div(n2, a);
   }
   if (t_min < temp1 && temp1 < t_max) tout = temp1;
   else if (t_min < temp2 && temp2 < t_max) tout = temp2;
@@ -240,8 +240,8 @@ __device__ __forceinline__ bool sphere_t12(V3 sc, double sr, const RayX& r, doub
   const double n1 = (-b) - sd, n2 = (-b) + sd;
   double temp1 = div_mk(n1, a, inva), temp2 = div_mk(n2, a, inva);
   if (!(in_range(a) & q_ok(n1, temp1) & q_ok(n2, temp2))) {
-    temp1 = n1 / a;
-    temp2 = n2 / a;
+    temp1 = ieee_div(n1, a);
+    temp2 = ieee_div(n2, a);
   }
   if (-INFINITY < temp1 && temp1 < INFINITY) t1 = temp1;
   else if (-INFINITY < temp2 && temp2 < INFINITY) t1 = temp2;
