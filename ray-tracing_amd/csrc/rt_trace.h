@@ -371,11 +371,6 @@ __device__ __forceinline__ bool prim_t(const Scene& S, const rt_node* n, const R
   if (type == RT_NODE_CUBOID) {
     if (RT_CUBOID_PRETEST && cuboid_missed(n->f, r, t_min, t_max)) return false;
     bool have = false;
-#if RT_CUBOID_UNROLL == 1
-#pragma unroll
-#elif RT_CUBOID_UNROLL == 2
-#pragma nounroll
-#endif
     for (int i = 5; i >= 0; --i) {
       int plane;
       double a0, a1, b0, b1, k, tt;

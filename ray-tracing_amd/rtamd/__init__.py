@@ -613,8 +613,10 @@ class Context:
     STEP_KINDS = ("box", "wide", "leaf", "medium", "frame")
 
     def step_profile(self, cam, params) -> dict:
-        """rt_render_step_profile: the binary / mixed walk's steps by the set of node kinds their lanes
-        were at: {"box+leaf": (ticks, steps), ...} (s_memtime ticks, counting build)."""
+        """rt_render_step_profile: the walk's steps by the set of node kinds their lanes were at:
+        {"box+leaf": (ticks, steps), ...} (s_memtime ticks, counting build). Binary and mixed walks: the kinds
+        of the lanes that stepped; the 4-wide walk (round 6): "wide" (node steps), "leaf" (leaf steps),
+        "box+wide" (node steps in which some lane walks a tie redo on the caller's tree)."""
         w, p = (C.c_uint64 * 16)(), (C.c_uint64 * 64)()
         _check(lib().rt_render_step_profile(self._h, C.byref(cam), C.byref(params), w, p), "rt_render_step_profile")
         out = {}

@@ -1,8 +1,7 @@
-# round-6 evidence, part 3: C5 profiles and bench line, the C4 parts probe, shard probes of C2 and C4
+# round 6: the step-profile test, C4 scheduling knobs re-swept on the final build
 cd "${GRAFT_REPO_ROOT:-.}" || exit 2
-scripts/gpu_round_profiles.sh r6 c5
-rc=$?; [ $rc -ge 124 ] && exit $rc
-scripts/gpu_steps.sh \
-  c4parts 300 "python -u scripts/c4_parts.py > gpurun_out/r6_c4_parts.txt" \
-  shard_c2 300 "python -u scripts/shard_probe.py --config c2 --shards 1 2 4 8 --reps 2 > gpurun_out/r6_shard_probe_c2.txt" \
-  shard_c4 400 "python -u scripts/shard_probe.py --config c4 --shards 1 8 --reps 2 > gpurun_out/r6_shard_probe_c4.txt"
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_scenes.py -m gpu -v --timeout 120 --timeout-method thread -rA -s -k step_profile > gpurun_out/r6_gpu_stepprof.log 2>&1
+rc=$?; echo "test rc=$rc"; [ $rc -ge 124 ] && exit $rc
+timeout -k 10 600 python -u scripts/ab.py time --bench="--config c4 --spp 100" --reps 2 . .:RTAMD_BOX_FIRST=2 .:RTAMD_BOX_FIRST=8 .:RTAMD_TRAV_STOP=4 .:RTAMD_TRAV_STOP=12 > gpurun_out/r6_ab_c4_knobs.log 2>&1
+echo "ab rc=$?"

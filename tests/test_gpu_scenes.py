@@ -216,3 +216,24 @@ def test_coplanar_ties(gpu_ctx, kind):
         assert redos == 0
     else:
         assert redos > 100  # (the camera rays through the overlap)
+
+
+@pytest.mark.parametrize("scene,camera,kinds", [
+    ("random_book_one", "random_scene", {"wide", "leaf", "box+wide"}),   # the 4-wide walk (round 6)
+    ("next_week_final", "next_week", None),                              # the mixed walk
+])
+def test_step_profile_bins(gpu_ctx, scene, camera, kinds):
+    """rt_render_step_profile (scripts/step_profile.py): every walk reports its
+    steps by kind with positive times. The 4-wide walk's steps are node steps, leaf steps, or node steps
+    with a tie redo on the caller's tree; the mixed walk of next_week_final has steps at instance frames."""
+    earth = np.load(os.path.join(os.path.dirname(__file__), "golden", "earthmap_rgb8.npz"))["rgb"]
+    sc, _ = rtamd.make_scene(scene, rtamd.randGen(1024), earth=earth if scene == "next_week_final" else None)
+    gpu_ctx.upload(sc)
+    cam = rtamd.camera(camera, 64, 48)
+    prof = gpu_ctx.step_profile(cam, rtamd.make_params(64, 48, 4, 50, rtamd.RT_RNG_PHILOX, seed=1024))
+    print(f"{scene} step profile: {prof}")
+    assert prof and all(ticks > 0 and n > 0 for ticks, n in prof.values())
+    if kinds is not None:
+        assert set(prof) <= kinds and {"wide", "leaf"} <= set(prof)
+    else:
+        assert any("frame" in k for k in prof) and any("wide" in k for k in prof)
