@@ -455,6 +455,11 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
   // (st: the lane's 6 LDS doubles, `stride` apart: throughput xyz, then the chunk's sum xyz)
   LaneV3<kStateLds<F>> thr{v3(0, 0, 0), st, stride};
   LaneV3<kSumLds<F>> sum{v3(0, 0, 0), st + 3 * (kSumLds<F> ? stride : 0), stride};
+  // (RT_LEAF_Q: the 4-wide walk's queue word sits below the lane's stack, rt_trace.h trav_postpone)
+  if constexpr (RT_LEAF_Q && (F & F_WIDE) != 0) {
+    stk[0] = (STK)-1;
+    stk += stride;
+  }
   RngPhilox g;
   g.init(A.seed, 0, 0);
   Trav t;  // the segment's ray lives only here between segments (no second copy is carried)
@@ -855,9 +860,13 @@ __global__ void assemble(const T* slabs, T* image, int W, int H, int tile, int t
 template <unsigned F>
 __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* rays, int n, double tmin,
                                                          double tmax, uint64_t seed, int joint, int walk, double* out) {
-  __shared__ int stk_mem[lane_ints<F>() * RT_BLOCK];
+  __shared__ int stk_mem[(lane_ints<F>() + 1) * RT_BLOCK];
   int* stk = &stk_mem[threadIdx.x];
-  Side side{&stk_mem[((F & (F_WIDE | F_MIXW)) ? RT_WSTACK : RT_STACK) * RT_BLOCK + threadIdx.x], RT_BLOCK};
+  Side side{&stk_mem[(((F & (F_WIDE | F_MIXW)) ? RT_WSTACK : RT_STACK) + 1) * RT_BLOCK + threadIdx.x], RT_BLOCK};
+  if constexpr (RT_LEAF_Q && (F & F_WIDE) != 0) {  // (the leaf queue word below the stack)
+    stk[0] = -1;
+    stk += RT_BLOCK;
+  }
   const int i = blockIdx.x * RT_BLOCK + threadIdx.x;
   if (i >= n) return;
   const double* q = rays + 7 * (long long)i;

@@ -509,7 +509,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   // LDS-staged kernel when the traversal's node array plus the stacks fit one CU's 160 KiB
   // (RTAMD_LDS=0 disables it for A/B runs).
   if (!count && !env_off("RTAMD_LDS") && (!is_full(var) || loop)) {
-    const int entries = wide ? c->wide_stack_need + 3 : c->stack_need + 2 + postpone;  // (wide_node writes 3 slots)
+    const int entries = wide ? c->wide_stack_need + 3 + (RT_LEAF_Q ? 1 : 0) : c->stack_need + 2 + postpone;  // (wide_node writes 3 slots; + the leaf queue word)
     const int items = wide ? c->n_wnodes : c->n_nodes;
     const size_t rec = wide ? sizeof(rt_wnode) : sizeof(rt_node);
     const bool leaf_lds = wide && !env_off("RTAMD_LEAF_LDS");  // RTAMD_LEAF_LDS=0: leaves never in LDS
@@ -557,7 +557,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   // 64-byte quantised form: A/B only, measured slower)
   const void* fn = philox_kernel(var, loop, false, count ? 1 : waves, count, false, loop == 2 && c->d_qnodes);
   // replacement loops: lane stacks (+ Side slots) in dynamic LDS, sized for this world's stack bound
-  int entries = wide ? c->wide_stack_need + 3 : c->stack_need + 2 + postpone;  // (wide_node writes 3 slots)
+  int entries = wide ? c->wide_stack_need + 3 + (RT_LEAF_Q ? 1 : 0) : c->stack_need + 2 + postpone;  // (wide_node writes 3 slots; + the leaf queue word)
   const size_t dyn = loop ? (size_t)(entries + side_ints) * RT_BLOCK * sizeof(int) : 0;
   if (loop) HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
   int bpc = 1;

@@ -1450,12 +1450,25 @@ template <class STK>
 __device__ __forceinline__ int trav_pop(Trav& t, const STK* stk, int stride) {
   return t.sp ? stk[(--t.sp) * stride] : kNone;
 }
-// node -> pend when node is a leaf and the slot is free, then continue with the next stack entry
+// A second postponed leaf per lane (RT_LEAF_Q=1, round 6, A/B): kept in the lane's LDS word just below its
+// stack (stk[-stride], -1 = empty; the kernels reserve it), filled only while `pend` holds one, so the walk
+// is over exactly when node and pend are. A lane then walks on past its second leaf instead of waiting for
+// the next leaf step.
+#ifndef RT_LEAF_Q
+#define RT_LEAF_Q 0
+#endif
+// node -> pend when node is a leaf and the slot is free (else the queue word), then continue with the
+// next stack entry
 template <class STK>
-__device__ __forceinline__ void trav_postpone(Trav& t, const STK* stk, int stride) {
-  if (t.node < 0 && t.node != kNone && t.pend < 0) {
-    t.pend = ~t.node;
-    t.node = trav_pop(t, stk, stride);
+__device__ __forceinline__ void trav_postpone(Trav& t, STK* stk, int stride) {
+  if (t.node < 0 && t.node != kNone) {
+    if (t.pend < 0) {
+      t.pend = ~t.node;
+      t.node = trav_pop(t, stk, stride);
+    } else if (RT_LEAF_Q && stk[-stride] < 0) {
+      stk[-stride] = (STK)~t.node;
+      t.node = trav_pop(t, stk, stride);
+    }
   }
 }
 template <unsigned F, class STK>
@@ -1467,10 +1480,17 @@ __device__ __forceinline__ void wide_inner(const Scene& S, Trav& t, STK* stk, in
 template <unsigned F, class R, class STK>
 __device__ __forceinline__ void wide_leaf(const Scene& S, Trav& t, double t_min, STK* stk, int stride, Cnt& cnt, R& g,
                                           Side& side) {
-  if (t.pend >= 0) {
+  // (RT_LEAF_Q=2: a lane holding two leaves tests both in one leaf step, one trav_leaf call site)
+#pragma nounroll
+  for (int k = 0; k < (RT_LEAF_Q == 2 ? 2 : 1) && t.pend >= 0; ++k) {
     const rt_node* n = &S.leaves[t.pend];  // (pend holds the leaf table slot)
     trav_leaf<F>(S, t, n, t.pend | kSlotTag, t_min, cnt, g, side, false);
-    t.pend = -1;
+    if (RT_LEAF_Q) {
+      t.pend = stk[-stride];
+      stk[-stride] = (STK)-1;
+    } else {
+      t.pend = -1;
+    }
   }
   trav_postpone(t, stk, stride);
 }
