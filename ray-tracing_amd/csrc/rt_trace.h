@@ -1453,7 +1453,8 @@ __device__ __forceinline__ int trav_pop(Trav& t, const STK* stk, int stride) {
 // A second postponed leaf per lane (RT_LEAF_Q=1, round 6, A/B): kept in the lane's LDS word just below its
 // stack (stk[-stride], -1 = empty; the kernels reserve it), filled only while `pend` holds one, so the walk
 // is over exactly when node and pend are. A lane then walks on past its second leaf instead of waiting for
-// the next leaf step.
+// the next leaf step. Measured slower (same images): C2 136.0 -> 138.5 ms, C5 at 64 spp 658 -> 670 ms; =2
+// (both leaves tested in one leaf step) 149.5 / 690 ms. Off.
 #ifndef RT_LEAF_Q
 #define RT_LEAF_Q 0
 #endif
