@@ -514,9 +514,10 @@ struct WideBuilder {
   // c_prim * area) or a wide node (c_node * area + the best spread of i's children over 4 slots).
   // pick[i][j] = how many of those slots the left child takes (0: j - 1 slots were as good).
   bool sah = false;
+  int K = RT_WIDE;  // child slots per wide node: 4, or 8 (a pair of 4-wide records, build_wide8_bvh)
   double c_node = 1.0, c_prim = 1.0;
-  std::vector<std::array<double, RT_WIDE + 1>> cost;
-  std::vector<std::array<int, RT_WIDE + 1>> pick;
+  std::vector<std::array<double, 2 * RT_WIDE + 1>> cost;
+  std::vector<std::array<int, 2 * RT_WIDE + 1>> pick;
   std::vector<char> done;
 
   double spread(int i, int j) {  // best split of internal node i's two children over j >= 2 slots
@@ -535,11 +536,11 @@ struct WideBuilder {
       if (!box_of(i, b)) { ok = false; return 0; }
       const double a = area(b);
       if (nodes[i].type != RT_NODE_BVH) {
-        for (int k = 1; k <= RT_WIDE; ++k) cost[i][k] = c_prim * a;
+        for (int k = 1; k <= K; ++k) cost[i][k] = c_prim * a;
       } else {
-        cost[i][1] = c_node * a + spread(i, RT_WIDE);
-        pick[i][1] = pick[i][RT_WIDE];  // (the wide node's own slots, see kids_sah)
-        for (int k = 2; k <= RT_WIDE; ++k) {
+        cost[i][1] = c_node * a + spread(i, K);
+        pick[i][1] = pick[i][K];  // (the wide node's own slots, see kids_sah)
+        for (int k = 2; k <= K; ++k) {
           const double c = spread(i, k);
           if (cost[i][k - 1] <= c) { cost[i][k] = cost[i][k - 1]; pick[i][k] = 0; }
           else cost[i][k] = c;
@@ -561,7 +562,7 @@ struct WideBuilder {
     std::vector<int> kids;
     const int k = pick[id][1];  // the split that cost[id][1] (a wide node at id) was priced with
     slots(nodes[id].a, k, kids);
-    slots(nodes[id].b, RT_WIDE - k, kids);
+    slots(nodes[id].b, K - k, kids);
     return kids;
   }
 
@@ -576,7 +577,7 @@ struct WideBuilder {
       if (!ok) return 0;
     }
     for (;;) {
-      if (sah || (int)kids.size() >= RT_WIDE) break;
+      if (sah || (int)kids.size() >= K) break;
       int best = -1;
       double best_area = -1;
       for (int k = 0; k < (int)kids.size(); ++k) {
@@ -592,36 +593,74 @@ struct WideBuilder {
       kids[best] = n.a;
       kids.insert(kids.begin() + best + 1, n.b);
     }
-    const int me = (int)out.size();
-    out.push_back(rt_wnode{});
+    // K = 8: the node is the record pair (2 me, 2 me + 1), its children ordered by box centre along the
+    // axis of the node's largest extent, the lower four in the first record; pad[0] of the first record
+    // holds that axis, so that a walk can take the half farther along the ray first (rt_trace.h wide_node8)
+    int order_axis = -1;
+    if (K == 2 * RT_WIDE) {
+      Box nb;
+      if (!box_of(id, nb)) { ok = false; return 0; }
+      order_axis = 0;
+      for (int a = 1; a < 3; ++a)
+        if (nb.mx[a] - nb.mn[a] > nb.mx[order_axis] - nb.mn[order_axis]) order_axis = a;
+      std::vector<std::pair<double, int>> keyed;
+      for (int kid : kids) {
+        Box b;
+        if (!box_of(kid, b)) { ok = false; return 0; }
+        keyed.push_back({b.mn[order_axis] + b.mx[order_axis], kid});
+      }
+      std::stable_sort(keyed.begin(), keyed.end(), [](const std::pair<double, int>& x, const std::pair<double, int>& y) {
+        return x.first < y.first;
+      });
+      // the lower half first: ceil(n / 2) children in the first record, the rest in the second
+      const int n = (int)keyed.size(), lo_n = (n + 1) / 2;
+      std::vector<int> sorted(2 * RT_WIDE, -1);
+      for (int k = 0; k < n; ++k) sorted[k < lo_n ? k : RT_WIDE + (k - lo_n)] = keyed[k].second;
+      kids = sorted;  // (-1: an unused slot)
+    }
+    const int recs = K / RT_WIDE;
+    const int me = (int)out.size() / recs;
+    for (int r = 0; r < recs; ++r) out.push_back(rt_wnode{});
+    int child_need = 0, used = 0;
+    for (int r = 0; r < recs; ++r) {
     rt_wnode w{};
-    int child_need = 0;
-    for (int k = 0; k < RT_WIDE; ++k) {
-      if (k >= (int)kids.size()) {
+    if (recs == 2) w.pad[0] = r == 0 ? order_axis : -1;
+    // (a pair's half: its first real child, for an unused slot's harmless leaf)
+    int first = -1;
+    for (int k = 0; k < RT_WIDE; ++k)
+      if (first < 0 && r * RT_WIDE + k < (int)kids.size() && kids[r * RT_WIDE + k] >= 0) first = kids[r * RT_WIDE + k];
+    if (first < 0)
+      for (int kid : kids)
+        if (kid >= 0) { first = kid; break; }
+    for (int kk = 0; kk < RT_WIDE; ++kk) {
+      const int k = r * RT_WIDE + kk;
+      if (k >= (int)kids.size() || kids[k] < 0) {
         // unused slot: an empty box (never accepted by a finite test) over a harmless leaf — the
         // first leaf below this node, re-testing which cannot change the closest hit — so that
         // rays accepting every child (fp32 slack = inf) need no slot check
-        for (int a = 0; a < 3; ++a) { w.lo[a][k] = INFINITY; w.hi[a][k] = -INFINITY; }
-        int leaf = kids[0];
+        for (int a = 0; a < 3; ++a) { w.lo[a][kk] = INFINITY; w.hi[a][kk] = -INFINITY; }
+        int leaf = first;
         while (nodes[leaf].type == RT_NODE_BVH) leaf = nodes[leaf].a;
-        w.child[k] = ~leaf;
+        w.child[kk] = ~leaf;
         continue;
       }
+      ++used;
       Box b;
       if (!box_of(kids[k], b)) { ok = false; return 0; }
-      for (int a = 0; a < 3; ++a) { w.lo[a][k] = f32_down(b.mn[a]); w.hi[a][k] = f32_up(b.mx[a]); }
+      for (int a = 0; a < 3; ++a) { w.lo[a][kk] = f32_down(b.mn[a]); w.hi[a][kk] = f32_up(b.mx[a]); }
       if (nodes[kids[k]].type == RT_NODE_BVH) {
         int cn = 0;
-        w.child[k] = build(kids[k], depth + 1, &cn);
+        w.child[kk] = build(kids[k], depth + 1, &cn);
         if (!ok) return 0;
         child_need = std::max(child_need, cn);
       } else {
-        w.child[k] = ~kids[k];
+        w.child[kk] = ~kids[k];
       }
     }
-    out[me] = w;
-    // the nearest hit child is entered, the other (<= 3) wait on the stack meanwhile
-    *need = (int)kids.size() - 1 + child_need;
+    out[recs * me + r] = w;
+    }
+    // the nearest hit child is entered, the others (<= K - 1) wait on the stack meanwhile
+    *need = used - 1 + child_need;
     return me;
   }
 };
@@ -644,6 +683,27 @@ bool build_wide_bvh(const std::vector<rt_node>& nodes, int root, std::vector<rt_
     b.pick.assign(nodes.size(), {});
     b.done.assign(nodes.size(), 0);
   }
+  b.build(root, 0, stack_need);
+  if (!b.ok) {
+    out.clear();
+    return false;
+  }
+  return true;
+}
+
+// The 8-wide collapse of the same tree (round 6, A/B: RTAMD_W8=1 at upload, spheres-only worlds): node p is
+// the record pair (2p, 2p + 1) of `out`, child ids >= 0 are pair indices. Same SAH-optimal programme with 8
+// child slots.
+bool build_wide8_bvh(const std::vector<rt_node>& nodes, int root, std::vector<rt_wnode>& out, int* stack_need) {
+  out.clear();
+  *stack_need = 0;
+  if (root < 0 || root >= (int)nodes.size() || nodes[root].type != RT_NODE_BVH) return false;
+  WideBuilder b{nodes, out};
+  b.sah = true;
+  b.K = 2 * RT_WIDE;
+  b.cost.assign(nodes.size(), {});
+  b.pick.assign(nodes.size(), {});
+  b.done.assign(nodes.size(), 0);
   b.build(root, 0, stack_need);
   if (!b.ok) {
     out.clear();

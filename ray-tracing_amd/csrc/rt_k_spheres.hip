@@ -3,7 +3,7 @@
 #include "rt_kernels.h"
 
 namespace rt {
-const void* philox_kernel_spheres(int loop, bool lds, int w, bool count, bool leaf_lds, bool q) {
-  return pick<kVarSpheres>(loop, lds, w, count, leaf_lds, q);
+const void* philox_kernel_spheres(int loop, bool lds, int w, bool count, bool leaf_lds, bool q, bool w8) {
+  return pick<kVarSpheres>(loop, lds, w, count, leaf_lds, q, w8);
 }
 }  // namespace rt

@@ -659,7 +659,7 @@ __device__ __forceinline__ void philox_loop2(const RenderArgs& A, const Scene& S
 // LDS ints per lane of a kernel: the traversal stack, then (instance frames possible) Side slots
 template <unsigned F>
 constexpr int lane_ints() {
-  return ((F & (F_WIDE | F_MIXW)) ? RT_WSTACK : RT_STACK) + ((F & F_FRAMES) ? kSideInts : 0);
+  return ((F & F_W8) ? 2 * RT_WSTACK : ((F & (F_WIDE | F_MIXW)) ? RT_WSTACK : RT_STACK)) + ((F & F_FRAMES) ? kSideInts : 0);
 }
 
 // Global-memory replacement loop: the lane stacks (and Side slots) in dynamic LDS sized by the host
@@ -862,7 +862,9 @@ __global__ void __launch_bounds__(RT_BLOCK) closest_hits(Scene S, const double* 
                                                          double tmax, uint64_t seed, int joint, int walk, double* out) {
   __shared__ int stk_mem[(lane_ints<F>() + 1) * RT_BLOCK];
   int* stk = &stk_mem[threadIdx.x];
-  Side side{&stk_mem[(((F & (F_WIDE | F_MIXW)) ? RT_WSTACK : RT_STACK) + 1) * RT_BLOCK + threadIdx.x], RT_BLOCK};
+  Side side{&stk_mem[(((F & F_W8) ? 2 * RT_WSTACK : ((F & (F_WIDE | F_MIXW)) ? RT_WSTACK : RT_STACK)) + 1) * RT_BLOCK +
+                     threadIdx.x],
+            RT_BLOCK};
   if constexpr (RT_LEAF_Q && (F & F_WIDE) != 0) {  // (the leaf queue word below the stack)
     stk[0] = -1;
     stk += RT_BLOCK;
@@ -1006,7 +1008,14 @@ __global__ void math_probe(int op, const double* x, const double* y, int n, doub
 // sample per lane walk, 1 = ray replacement over the binary tree, 2 = replacement over the
 // 4-wide tree.
 template <unsigned V>
-const void* pick_w(bool lds, int w, bool leaf_lds = false, bool q = false) {
+const void* pick_w(bool lds, int w, bool leaf_lds = false, bool q = false, bool w8 = false) {
+  if constexpr (V == (kVarSpheres | F_WIDE)) {
+    if (!lds && w8) {  // (the 8-wide tree as record pairs, from global memory: A/B)
+      if (w == 2) return (const void*)render_philox2<V | F_W8, 2>;
+      if (w == 4) return (const void*)render_philox2<V | F_W8, 4>;
+      return (const void*)render_philox2<V | F_W8, 3>;
+    }
+  }
   if constexpr (V == (kVarSpheres | F_WIDE)) {
     if (!lds && q) {  // (the quantised tree and sphere quadruples from global memory)
       if (w == 2) return (const void*)render_philox2<V | F_QNODE, 2>;
@@ -1040,15 +1049,16 @@ const void* pick_w(bool lds, int w, bool leaf_lds = false, bool q = false) {
   return (const void*)render_philox2<V, 1>;
 }
 template <unsigned V>
-const void* pick(int loop, bool lds, int w, bool count, bool leaf_lds, bool q = false) {
+const void* pick(int loop, bool lds, int w, bool count, bool leaf_lds, bool q = false, bool w8 = false) {
   if (count) {
     if constexpr (V == kVarSpheres) {
+      if (loop == 2 && w8) return (const void*)render_philox2<V | F_WIDE | F_COUNT | F_W8, 1>;
       if (loop == 2 && q) return (const void*)render_philox2<V | F_WIDE | F_COUNT | F_QNODE, 1>;
     }
     if (loop == 2) return (const void*)render_philox2<V | F_WIDE | F_COUNT, 1>;
     return loop ? (const void*)render_philox2<V | F_COUNT, 1> : (const void*)render_philox<V | F_COUNT, 1>;
   }
-  if (loop == 2) return pick_w<V | F_WIDE>(lds, w, leaf_lds, q);
+  if (loop == 2) return pick_w<V | F_WIDE>(lds, w, leaf_lds, q, w8);
   if (loop == 1) return pick_w<V>(lds, w);
   if (lds) {
     if (w == 2) return (const void*)render_philox_lds<V, 2>;
@@ -1079,7 +1089,7 @@ const void* pick_full(int loop, bool lds, int w, bool count) {
 // Render-kernel tables, one per kernel translation unit: the kernel for (loop, LDS-staged?, waves per
 // SIMD, counting build?, leaf table in LDS?) of that unit's variant(s).
 namespace rt {
-const void* philox_kernel_spheres(int loop, bool lds, int w, bool count, bool leaf_lds, bool q);
+const void* philox_kernel_spheres(int loop, bool lds, int w, bool count, bool leaf_lds, bool q, bool w8);
 const void* philox_kernel_cornell(int loop, bool lds, int w, bool count, bool leaf_lds);
 const void* philox_kernel_full(int loop, bool lds, int w, bool count);
 const void* philox_kernel_full_dark(int loop, bool lds, int w, bool count);

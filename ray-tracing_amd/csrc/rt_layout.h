@@ -66,8 +66,10 @@ enum : unsigned {
                    // (the oracle's too) instead of OCML
   F_QNODE = 4096u, // (spheres-only F_WIDE kernels reading the tree from global memory) the quantised 4-wide
                    // nodes (rt_qnode) and the leaves' sphere quadruples instead of the 128 / 64-byte records
-  F_SLEAF = 8192u  // (spheres-only F_WIDE kernels) leaf tests read the leaves' 32-byte sphere quadruples
+  F_SLEAF = 8192u, // (spheres-only F_WIDE kernels) leaf tests read the leaves' 32-byte sphere quadruples
                    // (Scene::sleaves, staged in LDS by the compact kernel) instead of the 64-byte records
+  F_W8 = 16384u    // (spheres-only F_WIDE kernels reading the tree from global memory; A/B, RTAMD_W8=1) an
+                   // 8-wide tree: node p is the 4-wide record pair (2p, 2p + 1), rt_bvh.cpp build_wide8_bvh
 };
 
 // Kernel variants: spheres-only (configs 1, 2, 5), Cornell-like (rects, instances, lights), full.

@@ -25,6 +25,7 @@ int rebuild_for_device(std::vector<rt_node>& nodes, int root);
 int unfold_media(std::vector<rt_node>& nodes, int root);
 bool build_wide_bvh(const std::vector<rt_node>& nodes, int root, std::vector<rt_wnode>& out, int* stack_need);
 bool quantize_wide(const std::vector<rt_wnode>& in, std::vector<rt_qnode>& out);
+bool build_wide8_bvh(const std::vector<rt_node>& nodes, int root, std::vector<rt_wnode>& out, int* stack_need);
 }  // namespace rt
 
 namespace rt {
@@ -434,8 +435,14 @@ int prepare_scene(const rt_scene_desc* din, uint32_t flags, PreparedScene& P) {
   if (P.replace_ok && !P.ref_walk) {  // 4-wide fp32-box tree over the same world tree (unflagged node copy)
     std::vector<rt_wnode> wide;
     int need = 0;
-    if (build_wide_bvh(nodes, d->world_root, wide, &need) && need + 3 <= RT_WSTACK &&
+    // RTAMD_W8=1 (A/B only): spheres-only worlds get the 8-wide tree as record pairs (F_W8 kernels; walked
+    // from global memory, 4 entries of stack headroom)
+    const char* w8env = std::getenv("RTAMD_W8");
+    const bool w8 = w8env && w8env[0] == '1' && variant_for(P.features) == kVarSpheres;
+    if ((w8 ? (build_wide8_bvh(nodes, d->world_root, wide, &need) && need + 4 <= 2 * RT_WSTACK)
+            : (build_wide_bvh(nodes, d->world_root, wide, &need) && need + 3 <= RT_WSTACK)) &&
         (size_t)wide.size() < (size_t)INT32_MAX / 2) {
+      P.w8 = w8;
       // The walk's leaf table: the leaves the wide tree references, each copied once (a moving
       // sphere with its EXT record), with `c` = the flat node id; leaf references ~id become ~slot.
       std::vector<rt_node> leaves;
@@ -465,7 +472,7 @@ int prepare_scene(const rt_scene_desc* din, uint32_t flags, PreparedScene& P) {
           for (int k = 0; k < 4; ++k) P.sleaves[4 * i + k] = leaves[i].f[k];
       }
       const char* qenv = std::getenv("RTAMD_QNODE");
-      if (!(spheres && qenv && qenv[0] == '1' && quantize_wide(wide, P.qnodes))) P.qnodes.clear();
+      if (w8 || !(spheres && qenv && qenv[0] == '1' && quantize_wide(wide, P.qnodes))) P.qnodes.clear();
       P.wnodes = std::move(wide);
       P.leaves = std::move(leaves);
       P.wide_stack_need = std::max(need, v.stack_need[unfolded]);

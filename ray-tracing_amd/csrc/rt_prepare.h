@@ -28,6 +28,7 @@ struct PreparedScene {
   int frame_depth = 0;            // deepest nesting of instance frames (the device tree's or the caller's)
   int wide_stack_need = 0;        // 4-wide walk stack bound
   bool rebuilt_bvh = false, mixed_wide = false, replace_ok = false, ref_walk = false;
+  bool w8 = false;                // wnodes hold the 8-wide tree as record pairs (RTAMD_W8=1, A/B; F_W8)
 };
 
 // Validates `desc` and prepares its device copy (RT_OK, or an error code with rt_last_error set).

@@ -59,6 +59,7 @@ struct rt_ctx {
   int n_leaves = 0;
   int n_wnodes = 0;
   int wide_stack_need = 0;
+  bool w8 = false;           // the 4-wide arrays hold the 8-wide tree as record pairs (F_W8 kernels, A/B)
   bool rebuilt_bvh = false;
   bool far_boxes = false;    // a BVH box coordinate beyond 2^100: the walks take the per-axis box test (cull())
   bool mixed_wide = false;   // media / frame world with 4-wide trees over its re-bounded subtrees (F_MIXW)
@@ -191,6 +192,7 @@ void free_scene(rt_ctx* c) {
   c->d_qnodes = nullptr;
   c->d_sleaves = nullptr;
   c->mixed_wide = false;
+  c->w8 = false;
   c->n_leaves = 0;
   c->n_wnodes = 0;
   c->d_nodes = nullptr;
@@ -256,8 +258,9 @@ int waves_target(int dflt) {
   return (w >= 1 && w <= 4) ? w : dflt;
 }
 // (the render kernels live in one translation unit per variant: rt_k_*.hip)
-const void* philox_kernel(unsigned var, int loop, bool lds, int w, bool count, bool leaf_lds = false, bool q = false) {
-  if (var == kVarSpheres) return rt::philox_kernel_spheres(loop, lds, w, count, leaf_lds, q);
+const void* philox_kernel(unsigned var, int loop, bool lds, int w, bool count, bool leaf_lds = false, bool q = false,
+                          bool w8 = false) {
+  if (var == kVarSpheres) return rt::philox_kernel_spheres(loop, lds, w, count, leaf_lds, q, w8);
   if (var == kVarCornell) return rt::philox_kernel_cornell(loop, lds, w, count, leaf_lds);
   if (var == kVarFullDark) return rt::philox_kernel_full_dark(loop, lds, w, count);
   return rt::philox_kernel_full(loop, lds, w, count);
@@ -508,7 +511,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   const int side_ints = side_ints_of(var, c->scene.frames, loop) + (lane_lds_of(var, loop) ? 4 : 0);
   // LDS-staged kernel when the traversal's node array plus the stacks fit one CU's 160 KiB
   // (RTAMD_LDS=0 disables it for A/B runs).
-  if (!count && !env_off("RTAMD_LDS") && (!is_full(var) || loop)) {
+  if (!count && !env_off("RTAMD_LDS") && (!is_full(var) || loop) && !(wide && c->w8)) {  // (F_W8: global only)
     const int entries = wide ? c->wide_stack_need + 3 + (RT_LEAF_Q ? 1 : 0) : c->stack_need + 2 + postpone;  // (wide_node writes 3 slots; + the leaf queue word)
     const int items = wide ? c->n_wnodes : c->n_nodes;
     const size_t rec = wide ? sizeof(rt_wnode) : sizeof(rt_node);
@@ -555,9 +558,11 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   }
   // (spheres-only worlds uploaded with RTAMD_QNODE=1 read the 4-wide tree from global memory in its
   // 64-byte quantised form: A/B only, measured slower)
-  const void* fn = philox_kernel(var, loop, false, count ? 1 : waves, count, false, loop == 2 && c->d_qnodes);
+  const void* fn = philox_kernel(var, loop, false, count ? 1 : waves, count, false, loop == 2 && c->d_qnodes,
+                                 loop == 2 && c->w8);
   // replacement loops: lane stacks (+ Side slots) in dynamic LDS, sized for this world's stack bound
-  int entries = wide ? c->wide_stack_need + 3 + (RT_LEAF_Q ? 1 : 0) : c->stack_need + 2 + postpone;  // (wide_node writes 3 slots; + the leaf queue word)
+  // (wide_node writes 3 slots, F_W8's farther half 4; + the leaf queue word)
+  int entries = wide ? c->wide_stack_need + (c->w8 ? 4 : 3) + (RT_LEAF_Q ? 1 : 0) : c->stack_need + 2 + postpone;
   const size_t dyn = loop ? (size_t)(entries + side_ints) * RT_BLOCK * sizeof(int) : 0;
   if (loop) HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
   int bpc = 1;
@@ -846,6 +851,7 @@ int upload_prepared(rt_ctx* c, const rt::PreparedScene& P, const rt_scene_desc* 
   c->n_leaves = (int)P.leaves.size();
   c->stack_need = P.stack_need;
   c->wide_stack_need = P.wide_stack_need;
+  c->w8 = P.w8;
   c->rebuilt_bvh = P.rebuilt_bvh;
   // The division-free box test (rt_trace.h box_hit) reads an infinite slab product as the quotient; with
   // |origin| <= 2^100 (ray_safe) and |d| >= 2^-900 that holds while every finite box coordinate is within
@@ -1117,7 +1123,10 @@ int rt_debug_closest_hits(rt_ctx* c, const double* rays, int n, double tmin, dou
   const dim3 grid((n + RT_BLOCK - 1) / RT_BLOCK);
   if ((flags & RT_DEBUG_QNODE) && !c->d_qnodes)
     return unsupported("rt_debug_closest_hits: no quantised 4-wide tree for this world (spheres-only worlds)");
-  if (flags & RT_DEBUG_QNODE)
+  if ((flags & RT_DEBUG_WIDE) && c->w8)  // (the 8-wide pairs: spheres-only worlds)
+    hipLaunchKernelGGL(closest_hits<F_UV | F_WIDE | F_W8>, grid, dim3(RT_BLOCK), 0, c->stream, c->scene, d_rays, n,
+                       tmin, tmax, seed, joint, 1, d_out);
+  else if (flags & RT_DEBUG_QNODE)
     hipLaunchKernelGGL(closest_hits<F_UV | F_WIDE | F_QNODE>, grid, dim3(RT_BLOCK), 0, c->stream, c->scene, d_rays, n,
                        tmin, tmax, seed, joint, 1, d_out);
   else if (flags & RT_DEBUG_WIDE)

@@ -1200,7 +1200,7 @@ __device__ __forceinline__ float4 qplanes(uint32_t q, float s, float o) {
 // others (farthest deepest). F_QNODE: the node is read in its quantised form (64 bytes) and its planes
 // decoded; the test over them is the same.
 template <unsigned F = 0, class STK>
-__device__ __forceinline__ bool wide_node(const Scene& S, Trav& t, STK* stk, int stride, int w) {
+__device__ __forceinline__ bool wide_node(const Scene& S, Trav& t, STK* stk, int stride, int w, bool all = false) {
   float4 nx, ny, nz, fx, fy, fz;
   int4 ch;
   if constexpr ((F & F_QNODE) != 0) {
@@ -1242,6 +1242,19 @@ __device__ __forceinline__ bool wide_node(const Scene& S, Trav& t, STK* stk, int
   cswap(k0, c0, k2, c2);
   cswap(k1, c1, k3, c3);
   cswap(k1, c1, k2, c2);
+  if ((F & F_W8) && all) {
+    // (F_W8's farther half: every accepted child stacked, farthest deepest, four slots written — the
+    // stacks have 4 entries of headroom under F_W8)
+    const int a0 = n_hit > 3 ? c3 : (n_hit > 2 ? c2 : (n_hit > 1 ? c1 : c0));
+    const int a1 = n_hit > 3 ? c2 : (n_hit > 2 ? c1 : c0);
+    const int a2 = n_hit > 3 ? c1 : c0;
+    stk[t.sp * stride] = a0;
+    stk[(t.sp + 1) * stride] = a1;
+    stk[(t.sp + 2) * stride] = a2;
+    stk[(t.sp + 3) * stride] = c0;
+    t.sp += n_hit;
+    return n_hit != 0;
+  }
   // Stack the accepted children after c0 without branches, farthest deepest: three slots are always
   // written (slots at or above the new sp are dead; the stacks have 3 entries of headroom for this).
   const int e0 = n_hit > 3 ? c3 : (n_hit > 2 ? c2 : c1);
@@ -1254,6 +1267,21 @@ __device__ __forceinline__ bool wide_node(const Scene& S, Trav& t, STK* stk, int
   return n_hit != 0;
 }
 
+// F_W8 (A/B; measured 1.8x slower on C5: the kernel spills and the 8-wide stack bound costs occupancy,
+// DESIGN.md §0 row 6): node p is the record pair (2p, 2p + 1), its children ordered along the axis in the first
+// record's pad[0] (rt_bvh.cpp build_wide8_bvh). The half farther along the ray on that axis is tested first
+// and every child it accepts stacked; then the nearer half's nearest accepted child is entered and its
+// others stacked above — or, with none, the walk pops (the farther half's nearest, if any).
+template <unsigned F, class STK>
+__device__ __forceinline__ bool wide_node8(const Scene& S, Trav& t, STK* stk, int stride, int p) {
+  const int ax = S.wnodes[2 * p].pad[0];
+  const bool neg = signbit(ax == 0 ? t.i32x : (ax == 1 ? t.i32y : t.i32z));
+  // (one inlined copy of the node test for both halves: a uniform loop)
+  bool in = false;
+#pragma nounroll
+  for (int h = 0; h < 2; ++h) in = wide_node<F>(S, t, stk, stride, 2 * p + ((h == 0) == neg ? 0 : 1), h == 0);
+  return in;
+}
 // Trav::node values of a walk with a postponed leaf (Trav::pend): nothing left but that leaf (kNone); or
 // the next stack entry closes an instance frame, which must wait until the leaf — found inside that frame,
 // in its ray's coordinates — is tested (kHold, the mixed walk).
@@ -1317,7 +1345,7 @@ __device__ __forceinline__ bool trav_step(const Scene& S, Trav& t, double t_min,
   if (wide) {
     if (t.node >= 0) {
       if constexpr ((F & F_COUNT) != 0) ++cnt.wide;
-      if (wide_node<F>(S, t, stk, stride, t.node)) return true;
+      if ((F & F_W8) ? wide_node8<F>(S, t, stk, stride, t.node) : wide_node<F>(S, t, stk, stride, t.node)) return true;
     } else {
       const rt_node* n = &S.leaves[~t.node];
       trav_leaf<F>(S, t, n, ~t.node | kSlotTag, t_min, cnt, g, side, false);
@@ -1475,7 +1503,10 @@ __device__ __forceinline__ void trav_postpone(Trav& t, STK* stk, int stride) {
 template <unsigned F, class STK>
 __device__ __forceinline__ void wide_inner(const Scene& S, Trav& t, STK* stk, int stride, Cnt& cnt) {
   if constexpr ((F & F_COUNT) != 0) ++cnt.wide;
-  if (!wide_node<F>(S, t, stk, stride, t.node)) t.node = trav_pop(t, stk, stride);
+  bool in;
+  if constexpr ((F & F_W8) != 0) in = wide_node8<F>(S, t, stk, stride, t.node);
+  else in = wide_node<F>(S, t, stk, stride, t.node);
+  if (!in) t.node = trav_pop(t, stk, stride);
   trav_postpone(t, stk, stride);
 }
 template <unsigned F, class R, class STK>

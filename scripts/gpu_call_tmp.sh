@@ -1,6 +1,8 @@
-# final-tree check: the GPU suite and smoke()
+# round 6: the 8-wide tree as record pairs (RTAMD_W8=1, A/B): image hashes against the default, then C5 timing
 cd "${GRAFT_REPO_ROOT:-.}" || exit 2
-scripts/gpu_steps.sh \
-  gputest_final 900 "python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -rA -s" \
-  smoke_final 300 "python -u -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'" \
-  bench_final 300 "python -u bench.py --steps 20 --warmup 5 > gpurun_out/r6_bench_c2_final.json"
+mkdir -p gpurun_out
+( timeout -k 10 120 python -u scripts/img_hash.py --config c5 --spp 2 && RTAMD_W8=1 timeout -k 10 120 python -u scripts/img_hash.py --config c5 --spp 2 && \
+  timeout -k 10 120 python -u scripts/img_hash.py --config c2 --spp 8 && RTAMD_W8=1 timeout -k 10 120 python -u scripts/img_hash.py --config c2 --spp 8 ) > gpurun_out/r6_w8_hash.log 2>&1
+rc=$?; echo "hash rc=$rc"; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 500 python -u scripts/ab.py time --bench="--config c5 --spp 64" --reps 2 . .:RTAMD_W8=1 > gpurun_out/r6_ab_c5_w8.log 2>&1
+echo "ab5 rc=$?"
