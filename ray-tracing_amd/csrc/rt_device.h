@@ -81,6 +81,16 @@ constexpr bool kSL = (F & F_SLIBM) != 0;
 // a - b*q is exact under FMA when nothing under- or overflows), then a range guard that falls back
 // to the IEEE division unless |a|, |b| and |q| all lie in [2^-900, 2^900] (zero, tiny, huge and
 // non-finite operands included). Bit-identical to `a / b` (tests/test_gpu_math.py).
+// A branch to a rare fallback (RT_COLD_BRANCHES=1, round 6, A/B): marked unlikely, so that block placement
+// moves the fallback out of the hot code's instruction-cache lines.
+#ifndef RT_COLD_BRANCHES
+#define RT_COLD_BRANCHES 0
+#endif
+#if RT_COLD_BRANCHES
+#define RT_COLD(c) __builtin_expect(!!(c), 0)
+#else
+#define RT_COLD(c) (c)
+#endif
 // The IEEE division of the rare operands. RT_DIV_CALL=1 puts it out of line, one copy per kernel instead of
 // one per inlined quotient (the C4 kernel inlines 157 IEEE divisions, ~1.9 k of its 14.1 k instructions, and
 // its 83.5 KB of code miss the instruction cache: 102 M misses per launch, profiles/r6_pmc_c4.json); the call
@@ -103,7 +113,7 @@ __device__ __forceinline__ double div_exact(double a, double b, double y) {
   q = fma(r, y, q);
   r = fma(-q, b, a);
   q = fma(r, y, q);
-  if (!(in_range(a) && in_range(b) && in_range(q))) q = ieee_div(a, b);
+  if (RT_COLD(!(in_range(a) && in_range(b) && in_range(q)))) q = ieee_div(a, b);
   return q;
 }
 
@@ -146,7 +156,7 @@ __device__ __forceinline__ double qdiv(double a, double d, double y) {
   q = fma(r, y, q);
   const bool zero = d == 0.0;
   q = zero ? a * y : q;
-  if (!(zero | (in_range(a) & in_range(d) & in_range(q)))) q = ieee_div(a, d);
+  if (RT_COLD(!(zero | (in_range(a) & in_range(d) & in_range(q))))) q = ieee_div(a, d);
   return q;
 }
 struct Hit {

@@ -163,7 +163,7 @@ __device__ __forceinline__ bool box_hit(const double* f, const RayX& r, double t
   const bool ok = ray_safe(r) & !nan;
   const bool yes = ok & ok_band & (U - L > band);
   const bool no = ok & ((ok_band & (L - U > band)) | (L == INFINITY) | (U == -INFINITY));
-  if (yes | no) return yes;
+  if (!RT_COLD(!(yes | no))) return yes;
   return box_hit_exact(f, r, t_min, t_max, true);
 }
 
@@ -216,7 +216,7 @@ __device__ __forceinline__ bool sphere_t(V3 sc, double sr, const RayX& r, double
   const double sd = sqrt(disc);
   const double n1 = (-b) - sd, n2 = (-b) + sd;
   double temp1 = div_mk(n1, a, inva), temp2 = div_mk(n2, a, inva);
-  if (!(in_range(a) & q_ok(n1, temp1) & q_ok(n2, temp2))) {
+  if (RT_COLD(!(in_range(a) & q_ok(n1, temp1) & q_ok(n2, temp2)))) {
     temp1 = ieee_div(n1, a);
     temp2 = ieee_div(n2, a);
   }
@@ -239,7 +239,7 @@ __device__ __forceinline__ bool sphere_t12(V3 sc, double sr, const RayX& r, doub
   const double sd = sqrt(disc);
   const double n1 = (-b) - sd, n2 = (-b) + sd;
   double temp1 = div_mk(n1, a, inva), temp2 = div_mk(n2, a, inva);
-  if (!(in_range(a) & q_ok(n1, temp1) & q_ok(n2, temp2))) {
+  if (RT_COLD(!(in_range(a) & q_ok(n1, temp1) & q_ok(n2, temp2)))) {
     temp1 = ieee_div(n1, a);
     temp2 = ieee_div(n2, a);
   }
