@@ -1090,6 +1090,7 @@ const void* pick_full(int loop, bool lds, int w, bool count) {
 // SIMD, counting build?, leaf table in LDS?) of that unit's variant(s).
 namespace rt {
 const void* philox_kernel_spheres(int loop, bool lds, int w, bool count, bool leaf_lds, bool q, bool w8);
+const void* philox_kernel_spheres_global(int w);  // rt_k_spheres_global.hip
 const void* philox_kernel_cornell(int loop, bool lds, int w, bool count, bool leaf_lds);
 const void* philox_kernel_full(int loop, bool lds, int w, bool count);
 const void* philox_kernel_full_dark(int loop, bool lds, int w, bool count);

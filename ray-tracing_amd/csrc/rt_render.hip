@@ -260,7 +260,11 @@ int waves_target(int dflt) {
 // (the render kernels live in one translation unit per variant: rt_k_*.hip)
 const void* philox_kernel(unsigned var, int loop, bool lds, int w, bool count, bool leaf_lds = false, bool q = false,
                           bool w8 = false) {
-  if (var == kVarSpheres) return rt::philox_kernel_spheres(loop, lds, w, count, leaf_lds, q, w8);
+  if (var == kVarSpheres) {
+    // (the 4-wide tree from global memory, 128-byte nodes: its own unit, rt_k_spheres_global.hip)
+    if (loop == 2 && !lds && !count && !q && !w8 && !std::getenv("RTAMD_NO_COLD")) return rt::philox_kernel_spheres_global(w);
+    return rt::philox_kernel_spheres(loop, lds, w, count, leaf_lds, q, w8);
+  }
   if (var == kVarCornell) return rt::philox_kernel_cornell(loop, lds, w, count, leaf_lds);
   if (var == kVarFullDark) return rt::philox_kernel_full_dark(loop, lds, w, count);
   return rt::philox_kernel_full(loop, lds, w, count);

@@ -1,6 +1,6 @@
 """Per-kernel register / scratch / occupancy table of the render kernels (hipcc -Rpass-analysis).
 
-    python scripts/resources.py [filter] [--tu spheres|cornell|full|full_dark|render ...] [-- extra hipcc flags]
+    python scripts/resources.py [filter] [--tu spheres|spheres_global|cornell|full|full_dark|render ...] [-- extra hipcc flags]
 
 The translation units (rt_k_*.hip, rt_render.hip) compile in parallel; --tu limits the run to some.
 """
@@ -17,7 +17,7 @@ def main():
     if "--" in args:
         i = args.index("--")
         args, extra = args[:i], args[i + 1:]
-    tus = ["spheres", "cornell", "full", "full_dark", "render"]
+    tus = ["spheres", "spheres_global", "cornell", "full", "full_dark", "render"]
     if "--tu" in args:
         i = args.index("--tu")
         sel = [a for a in args[i + 1:] if a in tus]
