@@ -1,8 +1,5 @@
-# round 6: the global spheres kernel from its own unit (cold-branch hints) against the spheres unit's (RTAMD_NO_COLD=1)
+# round 6: C5 evidence on the final build (rocprofv3 kernel stats, bench line)
 cd "${GRAFT_REPO_ROOT:-.}" || exit 2
-mkdir -p gpurun_out
-( timeout -k 10 120 python -u scripts/img_hash.py --config c5 --spp 2 && RTAMD_NO_COLD=1 timeout -k 10 120 python -u scripts/img_hash.py --config c5 --spp 2 ) > gpurun_out/r6_coldg_hash.log 2>&1
-rc=$?; echo "hash rc=$rc"; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 600 python -u scripts/ab.py time --bench="--config c5 --spp 64" --reps 3 . .:RTAMD_NO_COLD=1 > gpurun_out/r6_ab_coldg.log 2>&1
-rc=$?; echo "ab rc=$rc"; [ $rc -ge 124 ] && exit $rc
-scripts/gpu_steps.sh gputest_cold 900 "python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -x"
+scripts/gpu_steps.sh \
+  stats_c5 400 "cd /tmp && rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/gpurun_out/stats_c5b -o c5 -- python3 $PWD/bench.py --config c5 --steps 1 --warmup 0 --no-cpu-baseline --no-work" \
+  bench_c5 600 "python -u bench.py --config c5 --steps 1 --warmup 1 > gpurun_out/r6_bench_c5_final.json"
