@@ -83,7 +83,7 @@ constexpr bool kSL = (F & F_SLIBM) != 0;
 // non-finite operands included). Bit-identical to `a / b` (tests/test_gpu_math.py).
 // A branch to a rare fallback (RT_COLD_BRANCHES=1, round 6, A/B): marked unlikely, so that block placement
 // moves the fallback out of the hot code's instruction-cache lines. Measured: C5 -1.2 %, C2 +0.4 % (+8 B/lane of
-// scratch), C4 unchanged. Off.
+// scratch), C4 unchanged: on only in rt_k_spheres_global.hip (C5's kernel).
 #ifndef RT_COLD_BRANCHES
 #define RT_COLD_BRANCHES 0
 #endif
