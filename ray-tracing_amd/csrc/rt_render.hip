@@ -574,7 +574,7 @@ int launch_philox(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   const long long want = (A.work_total + RT_BLOCK - 1) / RT_BLOCK;
   const long long resident = (long long)c->cu_count * std::max(1, bpc);
   const int grid = (int)std::max(1ll, std::min(want, resident));
-  c->last_launch = rt_launch_info{var | (loop == 2 ? F_WIDE : 0u) | (count ? F_COUNT : 0u), loop, 0, 0,
+  c->last_launch = rt_launch_info{var | (loop == 2 ? F_WIDE : 0u) | (count ? F_COUNT : 0u) | (loop == 2 && c->w8 ? F_W8 : 0u), loop, 0, 0,
                                   count ? 1 : waves, grid, RT_BLOCK, (int)dyn, A.work_total, A.chunk,
                                   (loop == 2 || (loop == 1 && c->mixed_wide)) ? c->n_wnodes : 0, batches, 0};
   void* args[] = {&A, &entries};

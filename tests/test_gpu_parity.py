@@ -244,17 +244,18 @@ def _special_rays(sc, rng, n):
     return np.concatenate([o, d, rng.uniform(0, 1, (n, 1))], axis=1)
 
 
-@pytest.mark.parametrize("walk", [rtamd.RT_DEBUG_RESUMABLE, rtamd.RT_DEBUG_WIDE, rtamd.RT_DEBUG_QNODE])
+@pytest.mark.parametrize("walk", [rtamd.RT_DEBUG_RESUMABLE, rtamd.RT_DEBUG_WIDE, rtamd.RT_DEBUG_QNODE, "w8"])
 @pytest.mark.parametrize("name", ["random_book_one", "three_spheres", "cornell", "stress_spheres"])
 def test_resumable_walks_closest_hits(gpu_ctx, name, walk, monkeypatch):
     """The render loop's walks (binary resumable; 4-wide with conservative fp32 child boxes; the same
-    over the quantised 64-byte nodes and sphere quadruples of spheres-only worlds) give the oracle's
-    closest hits (the reference's makeBVH tree, fp64 slab tests) on random and adversarial rays: same
-    primitive, t, p, normal bit-identical."""
-    if walk == rtamd.RT_DEBUG_QNODE:
+    over the quantised 64-byte nodes and sphere quadruples of spheres-only worlds; the 8-wide tree as
+    4-wide record pairs, RTAMD_W8=1, A/B) give the oracle's closest hits (the reference's makeBVH tree,
+    fp64 slab tests) on random and adversarial rays: same primitive, t, p, normal bit-identical."""
+    if walk in (rtamd.RT_DEBUG_QNODE, "w8"):
         if name == "cornell":
-            pytest.skip("quantised trees are built for spheres-only worlds")
-        monkeypatch.setenv("RTAMD_QNODE", "1")  # (read at upload)
+            pytest.skip("quantised and 8-wide trees are built for spheres-only worlds")
+        monkeypatch.setenv("RTAMD_QNODE" if walk == rtamd.RT_DEBUG_QNODE else "RTAMD_W8", "1")  # (read at upload)
+        walk = rtamd.RT_DEBUG_QNODE if walk == rtamd.RT_DEBUG_QNODE else rtamd.RT_DEBUG_WIDE
     sc, _ = _scene(name, param=3000 if name == "stress_spheres" else 0)
     gpu_ctx.upload(sc)
     rng = np.random.default_rng(17)

@@ -237,3 +237,22 @@ def test_step_profile_bins(gpu_ctx, scene, camera, kinds):
         assert set(prof) <= kinds and {"wide", "leaf"} <= set(prof)
     else:
         assert any("frame" in k for k in prof) and any("wide" in k for k in prof)
+
+
+def test_w8_tree_renders_the_same_image(gpu_ctx, monkeypatch):
+    """The 8-wide tree as 4-wide record pairs (RTAMD_W8=1 at upload, F_W8 kernels; measured slower, A/B
+    only: DESIGN.md §3.2e) renders the 4-wide tree's image bit for bit: the closest hit does not depend on
+    the tree, exact ties aside, which both redo on the caller's tree."""
+    sc, _ = rtamd.make_scene("random_book_one", rtamd.randGen(1024))
+    cam = rtamd.camera("random_scene", 96, 64)
+    p = rtamd.make_params(96, 64, 8, 50, rtamd.RT_RNG_PHILOX, seed=1024)
+    gpu_ctx.upload(sc)
+    rgb_a, lin_a, _ = gpu_ctx.render(cam, p, linear=True)
+    monkeypatch.setenv("RTAMD_W8", "1")
+    info = rtamd.prepare_scene(sc)
+    gpu_ctx.upload(sc)
+    rgb_b, lin_b, _ = gpu_ctx.render(cam, p, linear=True)
+    launch = gpu_ctx.last_launch()
+    print(f"w8: {info['n_wide_nodes']} records, stack bound {info['wide_stack_need']}, launch {launch}")
+    assert launch["variant"] & 16384 and not launch["lds_staged"]  # (F_W8, from global memory)
+    assert np.array_equal(rgb_a, rgb_b) and np.array_equal(lin_a, lin_b, equal_nan=True)
