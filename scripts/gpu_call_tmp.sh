@@ -1,5 +1,5 @@
-# round 6: C3 walks re-measured: binary (default) vs 4-wide (RTAMD_WIDE=1); refill / box-first thresholds
+# final-tree check: the GPU suite and smoke()
 cd "${GRAFT_REPO_ROOT:-.}" || exit 2
-mkdir -p gpurun_out
-timeout -k 10 700 python -u scripts/ab.py time --bench="--config c3 --spp 300" --reps 2 . .:RTAMD_WIDE=1 .:RTAMD_TRAV_STOP=4 .:RTAMD_TRAV_STOP=16 > gpurun_out/r6_ab_c3_walks.log 2>&1
-echo "ab rc=$?"
+scripts/gpu_steps.sh \
+  gputest_final 900 "python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -rA -s" \
+  smoke_final 300 "python -u -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'"
