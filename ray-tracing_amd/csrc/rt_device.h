@@ -226,7 +226,15 @@ struct RngExactT {
 using RngExact = RngExactT<false>;
 
 // Tier B: Philox4x32-10, key = seed, counter = {pair, sample, pixel, 0}; two draws per block.
+// RT_PHILOX_OPAQUE_KEY=1 (round 6, A/B): the key is made opaque at each block (an empty asm on its scalar
+// registers), so that the 20 round keys are derived where a block is computed instead of being hoisted to the
+// kernel's entry and held (spilled to VGPR lanes and read back with v_readlane) across the whole loop.
+// Set by rt_k_spheres.hip only (C2 -0.35 %; C5 +0.5 %, C4 unchanged: DESIGN.md §3.1).
+#ifndef RT_PHILOX_OPAQUE_KEY
+#define RT_PHILOX_OPAQUE_KEY 0
+#endif
 __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+  if (RT_PHILOX_OPAQUE_KEY) asm volatile("" : "+s"(k0), "+s"(k1));
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     // one 32x32->64 multiply per word (v_mad_u64_u32) instead of separate mul_hi / mul_lo
