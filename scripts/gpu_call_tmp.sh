@@ -1,7 +1,13 @@
-# round-6 evidence for the final C2 kernel: GPU suite, smoke, C2 rocprofv3 stats + PMC + bench line
+# round 6: the camera read from the kernarg segment per sample (RT_CAM_KERNARG=1, _var_ck): hashes, C2, C5, C4
 cd "${GRAFT_REPO_ROOT:-.}" || exit 2
-scripts/gpu_steps.sh \
-  gputest_final 900 "python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -rA -s" \
-  smoke_final 300 "python -u -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'"
-rc=$?; [ $rc -ge 124 ] && exit $rc
-scripts/gpu_round_profiles.sh r6 c2 c1
+mkdir -p gpurun_out
+for d in . _var_ck; do
+  (cd $d && timeout -k 10 120 python -u scripts/img_hash.py --config c2 --spp 8 && timeout -k 10 120 python -u scripts/img_hash.py --config c4 --spp 4 && timeout -k 10 120 python -u scripts/img_hash.py --config c5 --spp 2) >> gpurun_out/r6_ck_hash.log 2>&1
+  rc=$?; echo "hash $d rc=$rc"; [ $rc -ne 0 ] && exit $rc
+done
+timeout -k 10 400 python -u scripts/ab.py time --reps 3 . _var_ck > gpurun_out/r6_ab_ck.log 2>&1
+rc=$?; echo "ab2 rc=$rc"; [ $rc -ge 124 ] && exit $rc
+timeout -k 10 400 python -u scripts/ab.py time --bench="--config c5 --spp 64" --reps 2 . _var_ck >> gpurun_out/r6_ab_ck.log 2>&1
+rc=$?; echo "ab5 rc=$rc"; [ $rc -ge 124 ] && exit $rc
+timeout -k 10 400 python -u scripts/ab.py time --bench="--config c4 --spp 100" --reps 3 . _var_ck >> gpurun_out/r6_ab_ck.log 2>&1
+echo "ab4 rc=$?"
