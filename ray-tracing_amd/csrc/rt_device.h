@@ -82,10 +82,10 @@ constexpr bool kSL = (F & F_SLIBM) != 0;
 // to the IEEE division unless |a|, |b| and |q| all lie in [2^-900, 2^900] (zero, tiny, huge and
 // non-finite operands included). Bit-identical to `a / b` (tests/test_gpu_math.py).
 // A branch to a rare fallback (RT_COLD_BRANCHES=1, round 6, A/B): marked unlikely, so that block placement
-// moves the fallback out of the hot code's instruction-cache lines. Measured: C5 -1.2 %, C2 +0.4 % (+8 B/lane of
-// scratch), C4 unchanged: on only in rt_k_spheres_global.hip (C5's kernel).
+// moves the fallback out of the hot code's instruction-cache lines. Measured (round 6, same images): C5 -1.2 %;
+// with the opaque Philox key (below) C2 -0.4 %, C3 -1.1 %, C4 ~-1 % (alone, C2 +0.4 %: +8 B/lane of scratch).
 #ifndef RT_COLD_BRANCHES
-#define RT_COLD_BRANCHES 0
+#define RT_COLD_BRANCHES 1
 #endif
 #if RT_COLD_BRANCHES
 #define RT_COLD(c) __builtin_expect(!!(c), 0)
@@ -229,7 +229,7 @@ using RngExact = RngExactT<false>;
 // RT_PHILOX_OPAQUE_KEY=1 (round 6, A/B): the key is made opaque at each block (an empty asm on its scalar
 // registers), so that the 20 round keys are derived where a block is computed instead of being hoisted to the
 // kernel's entry and held (spilled to VGPR lanes and read back with v_readlane) across the whole loop.
-// Set by rt_k_spheres.hip only (C2 -0.35 %; C5 +0.5 %, C4 unchanged: DESIGN.md §3.1).
+// Set by the spheres (C1, C2), Cornell (C3) and full-dark (C4) units; not by C5's (+0.5 % there): DESIGN.md §3.1.
 #ifndef RT_PHILOX_OPAQUE_KEY
 #define RT_PHILOX_OPAQUE_KEY 0
 #endif

@@ -1,9 +1,7 @@
 // rt_k_cornell.hip — render kernels of the Cornell-like variant (rects, instance chains, lights; config 3): one translation unit per variant, so
 // that the variants compile in parallel (rt_kernels.h).
-// The Philox key opaque per block and the rare-fallback branches marked unlikely (RT_PHILOX_OPAQUE_KEY,
-// RT_COLD_BRANCHES, rt_device.h): C3 at 300 spp 98.3-98.7 -> 97.2-97.6 ms, same images (round 6).
+// The Philox key opaque per block (RT_PHILOX_OPAQUE_KEY, rt_device.h; with the cold-branch hints, on everywhere): C3 at 300 spp 98.3-98.7 -> 97.2-97.6 ms, same images (round 6).
 #define RT_PHILOX_OPAQUE_KEY 1
-#define RT_COLD_BRANCHES 1
 #include "rt_kernels.h"
 
 namespace rt {

@@ -1,7 +1,5 @@
-# round-6 evidence for the final C3 / C4 kernels and the GPU suite
+# round 6: C2 with cold-branch hints on top of the opaque key (_var_c2cold)
 cd "${GRAFT_REPO_ROOT:-.}" || exit 2
-scripts/gpu_steps.sh \
-  gputest_final 900 "python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -rA -s" \
-  smoke_final 300 "python -u -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'"
-rc=$?; [ $rc -ge 124 ] && exit $rc
-scripts/gpu_round_profiles.sh r6 c4 c3
+mkdir -p gpurun_out
+timeout -k 10 400 python -u scripts/ab.py time --reps 4 . _var_c2cold > gpurun_out/r6_ab_c2cold.log 2>&1
+echo "ab rc=$?"
